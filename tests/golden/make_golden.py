@@ -1,0 +1,143 @@
+"""Generate the committed golden fixtures by running the REAL reference in this container.
+
+    python tests/golden/make_golden.py          (build container only: needs /root/reference)
+
+The reference is imported from /root/reference with placeholders for its absent third-party
+deps (`_ref_loader.py`), built from its own config file, loaded with the deterministic
+synthetic weights of `distilcodec_nabeel_amd.weights.synthetic_state_dict(seed=1234)`, put in
+eval mode, and run on CPU in fp32 with 8 torch threads.  Outputs are saved as small npz
+fixtures (inputs + expected outputs only; no reference source travels).
+
+Fixtures
+--------
+* `e2e_batch.npz`   : 2 ragged speech/music clips (1.00 s, 0.71 s) through `DistilCodec.encode`
+                      (raw_audio=True) and `quantizer.decode` + `generator` (the body of
+                      `decode_from_codes` with layout (G=1,B,T,R=1)); mel, encoder features,
+                      codes, x_pjt_in (clip 0), quantized, decoded waveform, fp64 top-2 VQ gaps.
+* `e2e_3s.npz`      : one 3 s speech clip, same stages (features omitted to keep it small).
+* `modules.npz`     : per-module cases called on the reference's own modules: ConvNeXtBlock(256),
+                      channels-first LayerNorm(256), ResBlock1(64, k=11), ParralelBlock(32),
+                      each ConvTranspose1d of the generator, EuclideanCodebook search on a
+                      1024-code slice.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+
+from distilcodec_nabeel_amd import synth, weights  # noqa: E402
+from oracle import reference_cpu as R  # noqa: E402  (fp64 gap analysis only)
+
+SEED = 1234
+THREADS = 8
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def build_reference():
+    import _ref_loader
+
+    dc = _ref_loader.import_reference()
+    cfg = json.load(open(os.path.join(_ref_loader.REF_ROOT, "configs", "model_config.json")))
+    codec = dc.DistilCodec(cfg)
+    sd = weights.synthetic_state_dict(cfg, seed=SEED)
+    for part in ("encoder", "quantizer", "generator"):
+        mod = getattr(codec, part)
+        tsd = {k: torch.from_numpy(v) for k, v in sd[part].items()}
+        missing, unexpected = mod.load_state_dict(tsd, strict=False)
+        allowed = {"grvq.rvqs.0.layers.0._codebook.embed_avg", "grvq.rvqs.0.layers.0._codebook.cluster_size"}
+        assert not unexpected, unexpected
+        assert set(missing) <= allowed, missing
+    codec.eval()
+    codec.device = torch.device("cpu")
+    return codec, cfg
+
+
+def run_e2e(codec, clips):
+    with torch.no_grad():
+        ret, gen_lens, hop_lens = codec.encode([[c, 24000] for c in clips], enable_bfloat16=False, raw_audio=True)
+        audios, mel, _, _ = codec.preprocess_raw_audio_batch([[c, 24000] for c in clips])
+        feat = codec.encoder(mel)
+        codes = ret.codes  # (1, B, T, 1)
+        z = codec.quantizer.decode(codes)
+        wav = codec.generator(z)
+    return dict(audio=_np(audios[:, 0]), mel=_np(mel), feat=_np(feat), codes=_np(codes[0, :, :, 0]).astype(np.int64),
+                x_pjt_in=_np(ret.x_pjt_in), quantized=_np(ret.quantized), z=_np(z), wav=_np(wav[:, 0]),
+                n_hop=np.array(hop_lens), gen_len=np.array(gen_lens),
+                tokens0=np.array([d["absolute_token_id"] for d in ret.codes_list[0]]))
+
+
+def main():
+    torch.manual_seed(0)
+    torch.set_num_threads(THREADS)
+    codec, cfg = build_reference()
+    embed = codec.quantizer.grvq.rvqs[0].layers[0]._codebook.embed[0]
+
+    clips = [synth.speech_like(24000, 11), synth.music_like(17000, 12)]
+    out = run_e2e(codec, clips)
+    best, second, arg64 = R.top2_gap_fp64(torch.from_numpy(out["x_pjt_in"]), embed)
+    out.update(gap_best=_np(best), gap_second=_np(second), argmin_fp64=_np(arg64).reshape(out["codes"].shape))
+    assert np.array_equal(out["z"], out["quantized"])  # decode(codes) == forward's up-path
+    out.pop("z")
+    out["x_pjt_in"] = out["x_pjt_in"][:1]  # clip 0 only: keeps the fixture small
+    out.update(threads=np.array(THREADS), seed=np.array(SEED))
+    np.savez_compressed(os.path.join(HERE, "e2e_batch.npz"), **out)
+    print("e2e_batch", {k: v.shape for k, v in out.items()})
+
+    out3 = run_e2e(codec, [synth.speech_like(72000, 21)])
+    best, second, arg64 = R.top2_gap_fp64(torch.from_numpy(out3["x_pjt_in"]), embed)
+    out3.update(gap_best=_np(best), gap_second=_np(second), argmin_fp64=_np(arg64).reshape(out3["codes"].shape))
+    for k in ("feat", "x_pjt_in", "z"):
+        out3.pop(k)
+    out3.update(threads=np.array(THREADS), seed=np.array(SEED))
+    np.savez_compressed(os.path.join(HERE, "e2e_3s.npz"), **out3)
+    print("e2e_3s", {k: v.shape for k, v in out3.items()})
+
+    # ---- per-module cases on the reference's own modules --------------------------------
+    g = np.random.Generator(np.random.PCG64(99))
+    mods = {}
+    with torch.no_grad():
+        blk = codec.encoder.stages[0][0]
+        x = torch.from_numpy(g.standard_normal((2, 256, 50), dtype=np.float32))
+        mods["convnext256_in"], mods["convnext256_out"] = _np(x), _np(blk(x))
+        ln = codec.encoder.downsample_layers[1][0]
+        mods["ln256_out"] = _np(ln(x))
+        rb = codec.generator.resblocks[3].blocks[2]  # ResBlock1(64, k=11, dil 1/3/5)
+        x = torch.from_numpy(g.standard_normal((2, 64, 300), dtype=np.float32))
+        mods["resblock64_in"], mods["resblock64_out"] = _np(x), _np(rb(x))
+        pb = codec.generator.resblocks[4]
+        x = torch.from_numpy(g.standard_normal((1, 32, 400), dtype=np.float32))
+        mods["parallel32_in"], mods["parallel32_out"] = _np(x), _np(pb(x))
+        for i, up in enumerate(codec.generator.ups):
+            x = torch.from_numpy(g.standard_normal((1, up.in_channels, 40), dtype=np.float32))
+            mods[f"ups{i}_in"], mods[f"ups{i}_out"] = _np(x), _np(up(x))
+        cb = codec.quantizer.grvq.rvqs[0].layers[0]._codebook
+        emb_small = embed[:1024].clone()
+        saved = cb.embed.data.clone()
+        cb.embed.data = emb_small[None]
+        cb.codebook_size = 1024
+        x = torch.from_numpy(out["x_pjt_in"][0, :64].copy())
+        q, ind, _ = cb(x[None])
+        cb.embed.data = saved
+        cb.codebook_size = embed.shape[0]
+        mods["vq1024_in"], mods["vq1024_codes"], mods["vq1024_quant"] = _np(x), _np(ind[0]).astype(np.int64), _np(q[0])
+        mods["mel_fb"] = _np(codec.spec_transform.fb)
+    np.savez_compressed(os.path.join(HERE, "modules.npz"), **mods)
+    print("modules", sorted(mods))
+    for f in ("e2e_batch.npz", "e2e_3s.npz", "modules.npz"):
+        print(f, os.path.getsize(os.path.join(HERE, f)) // 1024, "KiB")
+
+
+if __name__ == "__main__":
+    main()
