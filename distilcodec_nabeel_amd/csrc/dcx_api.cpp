@@ -1,0 +1,997 @@
+// Host runtime behind include/distilcodec_amd.h: checkpoint ingestion (weight-norm folding and
+// kernel-layout packing), workspace planning and stage orchestration on one HIP stream.
+//
+// Stage call graphs follow the reference modules (paths under the reference checkout):
+//   mel      mel_spec.py:26-57,100-122
+//   encode   encoders.py:68-76, convnext_utils.py:186-282
+//   vq       grfvq.py:105-146, residual_vq.py:103-259, vector_quantize_pytorch.py:41-45,462-538
+//   generate generators.py:118-147, convnext_utils.py:106-113,137-138
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/distilcodec_amd.h"
+#include "dcx_kernels.h"
+
+using dcx::ConvParams;
+
+namespace {
+
+struct HostTensor {
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+  int64_t numel() const {
+    int64_t n = 1;
+    for (auto s : shape) n *= s;
+    return n;
+  }
+};
+
+struct ConvW {
+  float* w = nullptr;
+  float* b = nullptr;
+  int cin = 0, cout = 0, taps = 1, phases = 1, in_step = 1, out_mul = 1;
+  int in_base[dcx::kMaxPhases] = {0};
+};
+
+struct LnW {
+  float* w = nullptr;
+  float* b = nullptr;
+  int C = 0;
+};
+
+struct BlockW {  // ConvNeXtBlock
+  int C = 0;
+  float *dww = nullptr, *dwb = nullptr, *gamma = nullptr;
+  LnW ln;
+  ConvW pw1, pw2;
+};
+
+struct Err {
+  int code;
+  std::string msg;
+};
+
+struct ProfRec {
+  int id;
+  int ev0, ev1;
+  double flops, bytes;
+};
+
+struct Bump {  // workspace carve-out, 256-byte aligned
+  char* base;
+  size_t cap, off = 0;
+  bool dry;
+  Bump(void* p, size_t c, bool d) : base((char*)p), cap(c), dry(d) {}
+  float* f(size_t n) { return (float*)raw(n * sizeof(float)); }
+  int* i(size_t n) { return (int*)raw(n * sizeof(int)); }
+  void* raw(size_t bytes) {
+    size_t o = (off + 255) & ~(size_t)255;
+    off = o + bytes;
+    return dry ? nullptr : base + o;
+  }
+  bool ok() const { return off <= cap; }
+};
+
+}  // namespace
+
+struct dcx_codec {
+  dcx_config cfg;
+  int device = 0;
+  std::string err;
+  std::map<std::string, HostTensor> host;
+  bool finalized = false, has_gen = false;
+  std::vector<void*> allocs;
+
+  ConvW dft, melfb;
+  ConvW stem;
+  LnW stem_ln, enc_norm;
+  LnW ds_ln[4];
+  ConvW ds_conv[4];
+  std::vector<BlockW> blocks[4];
+
+  ConvW vq_down, vq_pin, vq_up;
+  BlockW vq_down_blk, vq_up_blk;
+  float *codebook = nullptr, *e2 = nullptr, *ptable = nullptr;
+
+  ConvW conv_pre;
+  ConvW ups[8];
+  ConvW res[8][4][4][2];
+  float* post_w = nullptr;
+  float post_b = 0.f;
+
+  bool prof = false;
+  std::vector<hipEvent_t> events;
+  int ev_used = 0;
+  std::vector<ProfRec> pending;
+  std::vector<std::string> prof_names;
+  std::map<std::string, int> prof_ids;
+  std::vector<int64_t> prof_launches;
+  std::vector<double> prof_ms, prof_flops, prof_bytes;
+};
+
+namespace {
+
+int fail(dcx_codec* h, int code, const std::string& m) {
+  if (h) h->err = m;
+  return code;
+}
+
+#define HIPCHK(h, expr)                                                                   \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(h, DCX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+// ----------------------------------------------------------------------------------------
+// profiling
+// ----------------------------------------------------------------------------------------
+int prof_event(dcx_codec* h) {
+  if (h->ev_used == (int)h->events.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return -1;
+    h->events.push_back(e);
+  }
+  return h->ev_used++;
+}
+
+struct ProfScope {
+  dcx_codec* h;
+  hipStream_t s;
+  int e0 = -1;
+  ProfScope(dcx_codec* h_, hipStream_t s_) : h(h_), s(s_) {
+    if (h->prof) {
+      e0 = prof_event(h);
+      if (e0 >= 0) hipEventRecord(h->events[e0], s);
+    }
+  }
+  void done(const char* name, double flops, double bytes) {
+    if (!h->prof || e0 < 0) return;
+    int e1 = prof_event(h);
+    if (e1 < 0) return;
+    hipEventRecord(h->events[e1], s);
+    auto it = h->prof_ids.find(name);
+    int id;
+    if (it == h->prof_ids.end()) {
+      id = (int)h->prof_names.size();
+      h->prof_ids[name] = id;
+      h->prof_names.push_back(name);
+      h->prof_launches.push_back(0);
+      h->prof_ms.push_back(0);
+      h->prof_flops.push_back(0);
+      h->prof_bytes.push_back(0);
+    } else {
+      id = it->second;
+    }
+    h->pending.push_back({id, e0, e1, flops, bytes});
+  }
+};
+
+void prof_collect(dcx_codec* h) {
+  if (h->pending.empty()) return;
+  hipDeviceSynchronize();
+  for (auto& r : h->pending) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, h->events[r.ev0], h->events[r.ev1]);
+    h->prof_launches[r.id] += 1;
+    h->prof_ms[r.id] += ms;
+    h->prof_flops[r.id] += r.flops;
+    h->prof_bytes[r.id] += r.bytes;
+  }
+  h->pending.clear();
+  h->ev_used = 0;
+}
+
+// ----------------------------------------------------------------------------------------
+// weight ingestion
+// ----------------------------------------------------------------------------------------
+const HostTensor* find(dcx_codec* h, const std::string& k) {
+  auto it = h->host.find(k);
+  return it == h->host.end() ? nullptr : &it->second;
+}
+
+// Effective weight, folding weight norm (torch._weight_norm(v, g, dim=0)) in fp64.
+bool get_weight(dcx_codec* h, const std::string& prefix, HostTensor& out) {
+  if (auto t = find(h, prefix + ".weight")) {
+    out = *t;
+    return true;
+  }
+  const char* pairs[2][2] = {{".parametrizations.weight.original0", ".parametrizations.weight.original1"},
+                             {".weight_g", ".weight_v"}};
+  for (auto& pr : pairs) {
+    auto g = find(h, prefix + pr[0]);
+    auto v = find(h, prefix + pr[1]);
+    if (g && v) {
+      out.shape = v->shape;
+      out.data.resize(v->data.size());
+      const int64_t d0 = v->shape[0], inner = v->numel() / d0;
+      if ((int64_t)g->data.size() != d0) return false;
+      for (int64_t i = 0; i < d0; ++i) {
+        double nrm = 0;
+        for (int64_t j = 0; j < inner; ++j) nrm += (double)v->data[i * inner + j] * v->data[i * inner + j];
+        nrm = std::sqrt(nrm);
+        const double sc = (double)g->data[i] / nrm;
+        for (int64_t j = 0; j < inner; ++j) out.data[i * inner + j] = (float)(sc * v->data[i * inner + j]);
+      }
+      return true;
+    }
+  }
+  return false;
+}
+
+struct Builder {
+  dcx_codec* h;
+  Err e{DCX_OK, ""};
+
+  bool bad() const { return e.code != DCX_OK; }
+  void set(int c, const std::string& m) {
+    if (!bad()) e = {c, m};
+  }
+
+  float* upload(const std::vector<float>& v) {
+    if (bad()) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, v.size() * sizeof(float) + 16) != hipSuccess) {
+      set(DCX_ERR_OOM, "hipMalloc failed while uploading weights");
+      return nullptr;
+    }
+    h->allocs.push_back(p);
+    if (hipMemcpy(p, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+      set(DCX_ERR_HIP, "hipMemcpy failed while uploading weights");
+      return nullptr;
+    }
+    return (float*)p;
+  }
+  float* alloc(size_t n) {
+    if (bad()) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, n * sizeof(float) + 16) != hipSuccess) {
+      set(DCX_ERR_OOM, "hipMalloc failed");
+      return nullptr;
+    }
+    h->allocs.push_back(p);
+    return (float*)p;
+  }
+
+  const HostTensor* need(const std::string& k, std::vector<int64_t> shape) {
+    auto t = find(h, k);
+    if (!t) {
+      set(DCX_ERR_MISSING_WEIGHT, "missing checkpoint tensor '" + k + "'");
+      return nullptr;
+    }
+    if (t->numel() != [&] { int64_t n = 1; for (auto s : shape) n *= s; return n; }()) {
+      set(DCX_ERR_INVALID_ARG, "checkpoint tensor '" + k + "' has the wrong number of elements");
+      return nullptr;
+    }
+    return t;
+  }
+  float* vec(const std::string& k, int64_t n) {
+    auto t = need(k, {n});
+    return t ? upload(t->data) : nullptr;
+  }
+  HostTensor weight(const std::string& prefix, std::vector<int64_t> shape) {
+    HostTensor w;
+    if (bad()) return w;
+    if (!get_weight(h, prefix, w)) {
+      set(DCX_ERR_MISSING_WEIGHT, "missing checkpoint weight '" + prefix + "'");
+      return w;
+    }
+    int64_t n = 1;
+    for (auto s : shape) n *= s;
+    if (w.numel() != n) set(DCX_ERR_INVALID_ARG, "checkpoint weight '" + prefix + "' has the wrong shape");
+    return w;
+  }
+
+  // Conv1d / Linear weight [Cout][Cin][k] -> packed [Cout][k][Cin].
+  ConvW conv(const std::string& prefix, int cin, int cout, int k, int dil, int pad, bool has_bias = true) {
+    ConvW c;
+    c.cin = cin; c.cout = cout; c.taps = k; c.in_step = dil; c.in_base[0] = -pad;
+    HostTensor w = weight(prefix, {cout, cin, k});
+    if (bad()) return c;
+    std::vector<float> pk((size_t)cout * k * cin);
+    for (int o = 0; o < cout; ++o)
+      for (int i = 0; i < cin; ++i)
+        for (int j = 0; j < k; ++j) pk[((size_t)o * k + j) * cin + i] = w.data[((size_t)o * cin + i) * k + j];
+    c.w = upload(pk);
+    if (has_bias) c.b = vec(prefix + ".bias", cout);
+    return c;
+  }
+
+  // ConvTranspose1d weight [Cin][Cout][k], stride s, padding (k-s)/2 -> s polyphase convs:
+  // output o = q*s + r reads input q + base_r - m with tap j = (r+p)%s + m*s, m < k/s.
+  ConvW convT(const std::string& prefix, int cin, int cout, int k, int s) {
+    ConvW c;
+    const int p = (k - s) / 2, taps = k / s;
+    c.cin = cin; c.cout = cout; c.taps = taps; c.phases = s; c.in_step = -1; c.out_mul = s;
+    HostTensor w = weight(prefix, {cin, cout, k});
+    if (bad()) return c;
+    std::vector<float> pk((size_t)s * cout * taps * cin);
+    for (int r = 0; r < s; ++r) {
+      const int jr = (r + p) % s;
+      c.in_base[r] = (r + p - jr) / s;
+      for (int o = 0; o < cout; ++o)
+        for (int m = 0; m < taps; ++m)
+          for (int i = 0; i < cin; ++i)
+            pk[(((size_t)r * cout + o) * taps + m) * cin + i] = w.data[((size_t)i * cout + o) * k + jr + m * s];
+    }
+    c.w = upload(pk);
+    c.b = vec(prefix + ".bias", cout);
+    return c;
+  }
+
+  LnW ln(const std::string& prefix, int C) {
+    LnW l;
+    l.C = C;
+    l.w = vec(prefix + ".weight", C);
+    l.b = vec(prefix + ".bias", C);
+    return l;
+  }
+
+  BlockW block(const std::string& p, int C) {
+    BlockW b;
+    b.C = C;
+    auto dw = need(p + ".dwconv.weight", {C, 1, 7});
+    if (dw) {
+      std::vector<float> pk((size_t)7 * C);
+      for (int c = 0; c < C; ++c)
+        for (int j = 0; j < 7; ++j) pk[(size_t)j * C + c] = dw->data[(size_t)c * 7 + j];
+      b.dww = upload(pk);
+    }
+    b.dwb = vec(p + ".dwconv.bias", C);
+    b.ln = ln(p + ".norm", C);
+    b.pw1 = conv(p + ".pwconv1", C, 4 * C, 1, 1, 0);
+    b.pw2 = conv(p + ".pwconv2", 4 * C, C, 1, 1, 0);
+    b.gamma = vec(p + ".gamma", C);
+    return b;
+  }
+};
+
+// Slaney mel filterbank (torchaudio melscale_fbanks norm='slaney', mel_scale='slaney').
+double hz_to_mel(double f) {
+  const double f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp, logstep = std::log(6.4) / 27.0;
+  return f >= min_log_hz ? min_log_mel + std::log(f / min_log_hz) / logstep : f / f_sp;
+}
+double mel_to_hz(double m) {
+  const double f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp, logstep = std::log(6.4) / 27.0;
+  return m >= min_log_mel ? min_log_hz * std::exp(logstep * (m - min_log_mel)) : f_sp * m;
+}
+std::vector<double> mel_fb(int n_freqs, double fmin, double fmax, int n_mels, int sr) {
+  std::vector<double> fb((size_t)n_freqs * n_mels, 0.0);
+  std::vector<double> f_pts(n_mels + 2);
+  const double m0 = hz_to_mel(fmin), m1 = hz_to_mel(fmax);
+  for (int i = 0; i < n_mels + 2; ++i) f_pts[i] = mel_to_hz(m0 + (m1 - m0) * i / (n_mels + 1));
+  for (int k = 0; k < n_freqs; ++k) {
+    const double f = (double)(sr / 2) * k / (n_freqs - 1);
+    for (int m = 0; m < n_mels; ++m) {
+      const double down = (f - f_pts[m]) / (f_pts[m + 1] - f_pts[m]);
+      const double up = (f_pts[m + 2] - f) / (f_pts[m + 2] - f_pts[m + 1]);
+      double v = std::max(0.0, std::min(down, up));
+      v *= 2.0 / (f_pts[m + 2] - f_pts[m]);
+      fb[(size_t)k * n_mels + m] = v;
+    }
+  }
+  return fb;
+}
+
+int64_t frames_of(const dcx_config& c, int64_t n) {
+  const int64_t pad = (c.win - c.hop) / 2, padr = (c.win - c.hop + 1) / 2;
+  const int64_t len = n + pad + padr;
+  if (len < c.n_fft) return 0;
+  return (len - c.n_fft) / c.hop + 1;
+}
+
+int max_gen_width(const dcx_config& c) {  // max over generator layers of channels x (L / T)
+  int best = c.gen_channels, ch = c.gen_channels, up = 1;
+  for (int i = 0; i < c.n_ups; ++i) {
+    ch /= 2;
+    up *= c.up_rates[i];
+    best = std::max(best, ch * up);
+  }
+  return best;
+}
+
+// ----------------------------------------------------------------------------------------
+// launches
+// ----------------------------------------------------------------------------------------
+struct ConvCall {
+  const float* x;
+  long long x_bstride;
+  int batch, Lin, Lq, ldx;
+  float* y = nullptr;
+  float* y2 = nullptr;
+  float* macc = nullptr;
+  const float* res = nullptr;
+  const float* gamma = nullptr;
+  long long y_bstride = 0;
+  int ldy = 0;
+  int epi = dcx::EPI_BIAS, mean = dcx::MEAN_NONE;
+};
+
+int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s) {
+  ConvParams p{};
+  p.x = c.x;
+  p.w = w.w;
+  p.bias = w.b;
+  p.gamma = c.gamma;
+  p.res = c.res;
+  p.y = c.y;
+  p.y2 = c.y2;
+  p.macc = c.macc;
+  p.x_bstride = c.x_bstride;
+  p.ldy = c.ldy ? c.ldy : w.cout;
+  p.y_bstride = c.y_bstride ? c.y_bstride : (long long)c.Lq * w.out_mul * p.ldy;
+  p.w_phase_stride = (long long)w.cout * w.taps * w.cin;
+  p.Lin = c.Lin;
+  p.Lq = c.Lq;
+  p.Cin = w.cin;
+  p.Cout = w.cout;
+  p.ldx = c.ldx ? c.ldx : w.cin;
+  p.taps = w.taps;
+  p.in_step = w.in_step;
+  p.out_mul = w.out_mul;
+  for (int i = 0; i < dcx::kMaxPhases; ++i) p.in_base[i] = w.in_base[i];
+  p.epi = c.epi;
+  p.mean_mode = c.mean;
+  ProfScope ps(h, s);
+  const char* kname = "conv";
+  HIPCHK(h, dcx::launch_conv(p, c.batch, w.phases, s, &kname));
+  const double outs = (double)c.batch * c.Lq * w.phases * w.cout;
+  ps.done(kname, 2.0 * outs * w.cin * w.taps,
+          4.0 * ((double)c.batch * c.Lin * w.cin + outs + (double)w.phases * w.cout * w.taps * w.cin));
+  return DCX_OK;
+}
+
+// Pointwise conv / Linear over all B*T rows at once.
+int run_pointwise(dcx_codec* h, const ConvW& w, const float* x, long long rows, float* y, hipStream_t s,
+                  int epi = dcx::EPI_BIAS, const float* res = nullptr, const float* gamma = nullptr) {
+  ConvCall c{x, 0, 1, (int)rows, (int)rows, 0};
+  c.y = y;
+  c.res = res;
+  c.gamma = gamma;
+  c.epi = epi;
+  return run_conv(h, w, c, s);
+}
+
+#define RUN(expr)             \
+  do {                        \
+    int rc_ = (expr);         \
+    if (rc_ != DCX_OK) return rc_; \
+  } while (0)
+
+#define LAUNCH(h, s, name, flops, bytes, expr) \
+  do {                                         \
+    ProfScope ps_(h, s);                       \
+    HIPCHK(h, expr);                           \
+    ps_.done(name, flops, bytes);              \
+  } while (0)
+
+// ConvNeXtBlock in place on x [B][T][C]; ln: [M][C] scratch, hid: [M][4C] scratch.
+int run_block(dcx_codec* h, const BlockW& bw, float* x, int B, int T, float* ln, float* hid, hipStream_t s) {
+  const long long M = (long long)B * T;
+  const int C = bw.C;
+  LAUNCH(h, s, "dwconv_ln", 14.0 * M * C, 8.0 * M * C,
+         dcx::launch_dwconv_ln(x, ln, bw.dww, bw.dwb, bw.ln.w, bw.ln.b, B, T, C, s));
+  RUN(run_pointwise(h, bw.pw1, ln, M, hid, s, dcx::EPI_GELU));
+  RUN(run_pointwise(h, bw.pw2, hid, M, x, s, dcx::EPI_GAMMA_RES, x, bw.gamma));
+  return DCX_OK;
+}
+
+int run_ln(dcx_codec* h, const LnW& l, const float* x, float* y, long long rows, hipStream_t s) {
+  LAUNCH(h, s, "ln_rows", 8.0 * rows * l.C, 8.0 * rows * l.C,
+         dcx::launch_ln_rows(x, y, l.w, l.b, rows, l.C, 1e-6f, 1, s));
+  return DCX_OK;
+}
+
+// ---------------- stage bodies (dry=true only sizes the workspace) ----------------
+int stage_mel(dcx_codec* h, const float* audio, int B, int64_t n, float* mel, Bump& ws, hipStream_t s) {
+  const dcx_config& c = h->cfg;
+  const int T = (int)frames_of(c, n);
+  const int rows = T + c.n_fft / c.hop - 1;
+  float* fr = ws.f((size_t)B * rows * c.hop);
+  float* spec = ws.f((size_t)B * T * h->dft.cout);
+  float* mag = ws.f((size_t)B * T * h->melfb.cin);
+  if (ws.dry) return DCX_OK;
+  if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for mel");
+  LAUNCH(h, s, "frame_pad", 0, 8.0 * B * rows * c.hop,
+         dcx::launch_frame_pad(audio, fr, B, n, rows, c.hop, (c.win - c.hop) / 2, s));
+  ConvCall cc{fr, (long long)rows * c.hop, B, rows, T, c.hop};
+  cc.y = spec;
+  RUN(run_conv(h, h->dft, cc, s));
+  const int nbins = c.n_fft / 2 + 1;
+  LAUNCH(h, s, "spec_mag", 4.0 * B * T * nbins, 4.0 * B * T * (h->dft.cout + h->melfb.cin),
+         dcx::launch_spec_mag(spec, mag, (long long)B * T, nbins, h->melfb.cin, s));
+  RUN(run_pointwise(h, h->melfb, mag, (long long)B * T, mel, s, dcx::EPI_LOGCLAMP));
+  return DCX_OK;
+}
+
+int stage_encode(dcx_codec* h, const float* mel, int B, int T, float* feat, Bump& ws, hipStream_t s) {
+  const dcx_config& c = h->cfg;
+  const long long M = (long long)B * T;
+  const int cmax = c.enc_dims[3];
+  float* xa = ws.f((size_t)M * cmax);
+  float* xb = ws.f((size_t)M * cmax);
+  float* hid = ws.f((size_t)M * 4 * cmax);
+  if (ws.dry) return DCX_OK;
+  if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for encode");
+  ConvCall cc{mel, (long long)T * c.n_mels, B, T, T, c.n_mels};
+  cc.y = xa;
+  RUN(run_conv(h, h->stem, cc, s));
+  RUN(run_ln(h, h->stem_ln, xa, xb, M, s));
+  for (int i = 0; i < 4; ++i) {
+    if (i > 0) {
+      RUN(run_ln(h, h->ds_ln[i], xb, xa, M, s));
+      RUN(run_pointwise(h, h->ds_conv[i], xa, M, xb, s));
+    }
+    for (auto& bw : h->blocks[i]) RUN(run_block(h, bw, xb, B, T, xa, hid, s));
+  }
+  RUN(run_ln(h, h->enc_norm, xb, feat, M, s));
+  return DCX_OK;
+}
+
+int stage_vq_encode(dcx_codec* h, const float* feat, int B, int T, int32_t* codes, float* pin, float* fup,
+                    float* quant, Bump& ws, hipStream_t s) {
+  const dcx_config& c = h->cfg;
+  const long long M = (long long)B * T;
+  const int D = c.vq_dim, CD = c.codebook_dim, NC = c.codebook_size;
+  const int ntiles = dcx::vq_argmin_ntiles(NC);
+  float* x = ws.f((size_t)M * D);
+  float* ln = ws.f((size_t)M * D);
+  float* hid = ws.f((size_t)M * 4 * D);
+  float* P = pin ? pin : ws.f((size_t)M * CD);
+  float* x2 = ws.f((size_t)M);
+  float* pv = ws.f((size_t)M * ntiles);
+  int* pi = ws.i((size_t)M * ntiles);
+  float* zd = ws.f((size_t)M * D);
+  if (ws.dry) return DCX_OK;
+  if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for vq_encode");
+  RUN(run_pointwise(h, h->vq_down, feat, M, x, s));
+  RUN(run_block(h, h->vq_down_blk, x, B, T, ln, hid, s));
+  RUN(run_pointwise(h, h->vq_pin, x, M, P, s));
+  LAUNCH(h, s, "row_sqnorm", 2.0 * M * CD, 4.0 * M * CD, dcx::launch_row_sqnorm(P, M, CD, x2, s));
+  {
+    ConvParams p{};
+    p.x = P; p.w = h->codebook; p.Cin = CD; p.Cout = NC; p.ldx = CD; p.taps = 1; p.in_step = 1; p.out_mul = 1;
+    p.x2 = x2; p.e2 = h->e2; p.part_val = pv; p.part_idx = pi;
+    ProfScope ps(h, s);
+    const char* kname = "vq";
+    HIPCHK(h, dcx::launch_vq_argmin(p, (int)M, s, &kname));
+    ps.done(kname, 2.0 * M * NC * CD, 4.0 * ((double)M * CD + (double)NC * CD));
+  }
+  LAUNCH(h, s, "vq_reduce", 0, 8.0 * M * ntiles, dcx::launch_vq_reduce(pv, pi, (int)M, ntiles, codes, s));
+  if (fup) LAUNCH(h, s, "gather_rows", 0, 8.0 * M * CD, dcx::launch_gather_rows(h->codebook, NC, codes, M, CD, fup, nullptr, s));
+  if (quant) {
+    LAUNCH(h, s, "gather_rows", 0, 8.0 * M * D, dcx::launch_gather_rows(h->ptable, NC, codes, M, D, zd, nullptr, s));
+    RUN(run_pointwise(h, h->vq_up, zd, M, quant, s));
+    RUN(run_block(h, h->vq_up_blk, quant, B, T, ln, hid, s));
+  }
+  return DCX_OK;
+}
+
+int stage_vq_decode(dcx_codec* h, const int32_t* codes, int B, int T, float* z, int32_t* n_invalid, Bump& ws,
+                    hipStream_t s) {
+  const dcx_config& c = h->cfg;
+  const long long M = (long long)B * T;
+  const int D = c.vq_dim;
+  float* zd = ws.f((size_t)M * D);
+  float* ln = ws.f((size_t)M * D);
+  float* hid = ws.f((size_t)M * 4 * D);
+  if (ws.dry) return DCX_OK;
+  if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for vq_decode");
+  LAUNCH(h, s, "gather_rows", 0, 8.0 * M * D,
+         dcx::launch_gather_rows(h->ptable, c.codebook_size, codes, M, D, zd, n_invalid, s));
+  RUN(run_pointwise(h, h->vq_up, zd, M, z, s));
+  RUN(run_block(h, h->vq_up_blk, z, B, T, ln, hid, s));
+  return DCX_OK;
+}
+
+int stage_generate(dcx_codec* h, const float* z, int B, int T, float* wav, Bump& ws, hipStream_t s) {
+  const dcx_config& c = h->cfg;
+  const size_t per = (size_t)B * T * max_gen_width(c);
+  float* S = ws.f(per);
+  float* X = ws.f(per);
+  float* XS = ws.f(per);
+  float* R = ws.f(per);
+  float* RS = ws.f(per);
+  float* Tb = ws.f(per);
+  if (ws.dry) return DCX_OK;
+  if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for generate");
+  int C = c.gen_channels, L = T;
+  {  // conv_pre, then the first stage's SiLU (generators.py:121,125) fused as the only output
+    ConvCall cc{z, (long long)T * c.vq_dim, B, T, T, c.vq_dim};
+    cc.y2 = S;
+    RUN(run_conv(h, h->conv_pre, cc, s));
+  }
+  for (int i = 0; i < c.n_ups; ++i) {
+    const ConvW& up = h->ups[i];
+    const int Co = up.cout, Lo = L * c.up_rates[i];
+    {
+      ConvCall cc{S, (long long)L * C, B, L, L, C};
+      cc.y = X;
+      cc.y2 = XS;
+      RUN(run_conv(h, up, cc, s));
+    }
+    for (int rb = 0; rb < c.n_res; ++rb) {
+      for (int ci = 0; ci < 3; ++ci) {
+        const float* src = ci == 0 ? XS : RS;
+        const float* resid = ci == 0 ? X : R;
+        {
+          ConvCall cc{src, (long long)Lo * Co, B, Lo, Lo, Co};
+          cc.y2 = Tb;
+          RUN(run_conv(h, h->res[i][rb][ci][0], cc, s));
+        }
+        ConvCall cc{Tb, (long long)Lo * Co, B, Lo, Lo, Co};
+        cc.epi = dcx::EPI_RES;
+        cc.res = resid;
+        if (ci < 2) {
+          cc.y = R;
+          cc.y2 = RS;
+        } else {
+          cc.macc = S;
+          cc.mean = rb == 0 ? dcx::MEAN_FIRST : (rb == c.n_res - 1 ? dcx::MEAN_LAST : dcx::MEAN_MID);
+          if (rb == c.n_res - 1) cc.y2 = S;  // silu(mean): consumed by ups[i+1] / conv_post
+        }
+        RUN(run_conv(h, h->res[i][rb][ci][1], cc, s));
+      }
+    }
+    C = Co;
+    L = Lo;
+  }
+  LAUNCH(h, s, "conv_post_tanh", 2.0 * B * L * C * c.gen_post_k, 4.0 * B * L * (C + 1),
+         dcx::launch_conv_post_tanh(S, h->post_w, h->post_b, wav, B, L, C, c.gen_post_k, s));
+  return DCX_OK;
+}
+
+int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int32_t* codes, float* wav, Bump& ws,
+                        hipStream_t s) {
+  const dcx_config& c = h->cfg;
+  const int T = (int)frames_of(c, n);
+  const long long M = (long long)B * T;
+  float* mel = ws.f((size_t)M * c.n_mels);
+  float* feat = ws.f((size_t)M * c.enc_dims[3]);
+  float* z = ws.f((size_t)M * c.vq_dim);
+  const size_t mark = ws.off;
+  size_t need = mark;
+  auto sub = [&](auto fn) -> int {  // each sub-stage reuses the tail of the workspace
+    Bump tail(ws.base, ws.cap, ws.dry);
+    tail.off = mark;
+    int rc = fn(tail);
+    need = std::max(need, tail.off);
+    return rc;
+  };
+  if (ws.dry) {
+    sub([&](Bump& t) { return stage_mel(h, audio, B, n, mel, t, s); });
+    sub([&](Bump& t) { return stage_encode(h, mel, B, T, feat, t, s); });
+    sub([&](Bump& t) { return stage_vq_encode(h, feat, B, T, codes, nullptr, nullptr, nullptr, t, s); });
+    sub([&](Bump& t) { return stage_vq_decode(h, codes, B, T, z, nullptr, t, s); });
+    sub([&](Bump& t) { return stage_generate(h, z, B, T, wav, t, s); });
+    ws.off = need;
+    return DCX_OK;
+  }
+  if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for encode_decode");
+  RUN(sub([&](Bump& t) { return stage_mel(h, audio, B, n, mel, t, s); }));
+  RUN(sub([&](Bump& t) { return stage_encode(h, mel, B, T, feat, t, s); }));
+  RUN(sub([&](Bump& t) { return stage_vq_encode(h, feat, B, T, codes, nullptr, nullptr, nullptr, t, s); }));
+  RUN(sub([&](Bump& t) { return stage_vq_decode(h, codes, B, T, z, nullptr, t, s); }));
+  RUN(sub([&](Bump& t) { return stage_generate(h, z, B, T, wav, t, s); }));
+  return DCX_OK;
+}
+
+int check_ready(dcx_codec* h, bool need_gen) {
+  if (!h) return DCX_ERR_INVALID_ARG;
+  if (!h->finalized) return fail(h, DCX_ERR_STATE, "dcx_finalize has not been called");
+  if (need_gen && !h->has_gen) return fail(h, DCX_ERR_STATE, "generator weights were not finalized");
+  int dev = -1;
+  hipGetDevice(&dev);
+  if (dev != h->device) return fail(h, DCX_ERR_STATE, "handle belongs to another HIP device");
+  return DCX_OK;
+}
+
+}  // namespace
+
+// =========================================================================================
+// C ABI
+// =========================================================================================
+extern "C" {
+
+int dcx_abi_version(void) { return DCX_ABI_VERSION; }
+
+const char* dcx_status_string(int st) {
+  switch (st) {
+    case DCX_OK: return "ok";
+    case DCX_ERR_INVALID_ARG: return "invalid argument";
+    case DCX_ERR_MISSING_WEIGHT: return "missing weight";
+    case DCX_ERR_STATE: return "invalid state";
+    case DCX_ERR_HIP: return "HIP error";
+    case DCX_ERR_OOM: return "out of device memory";
+    case DCX_ERR_WORKSPACE: return "workspace too small";
+    default: return "unknown status";
+  }
+}
+
+void dcx_default_config(dcx_config* c) {
+  std::memset(c, 0, sizeof(*c));
+  c->sample_rate = 24000;
+  c->n_fft = 1024; c->hop = 256; c->win = 1024; c->n_mels = 128;
+  c->f_min = 0.f; c->f_max = 12000.f;
+  const int dep[4] = {3, 3, 9, 3}, dim[4] = {256, 512, 768, 1024};
+  for (int i = 0; i < 4; ++i) { c->enc_depths[i] = dep[i]; c->enc_dims[i] = dim[i]; }
+  c->vq_dim = 1024; c->codebook_dim = 3584; c->codebook_size = 32768;
+  c->gen_channels = 1024; c->gen_pre_k = 13; c->gen_post_k = 13;
+  c->n_ups = 5;
+  const int ur[5] = {8, 4, 2, 2, 2}, uk[5] = {16, 12, 4, 4, 4};
+  for (int i = 0; i < 5; ++i) { c->up_rates[i] = ur[i]; c->up_kernels[i] = uk[i]; }
+  c->n_res = 3;
+  const int rk[3] = {3, 7, 11};
+  for (int i = 0; i < 3; ++i) {
+    c->res_kernels[i] = rk[i];
+    c->res_dilations[i][0] = 1; c->res_dilations[i][1] = 3; c->res_dilations[i][2] = 5;
+  }
+}
+
+const char* dcx_last_error(const dcx_codec* h) { return h ? h->err.c_str() : "null handle"; }
+
+int dcx_create(const dcx_config* cfg, dcx_codec** out) {
+  if (!cfg || !out) return DCX_ERR_INVALID_ARG;
+  *out = nullptr;
+  const dcx_config& c = *cfg;
+  bool ok = c.n_fft == 1024 && c.win == 1024 && c.hop == 256 && c.n_mels % 16 == 0 && c.n_mels > 0 &&
+            c.vq_dim == c.enc_dims[3] && c.codebook_dim % 16 == 0 && c.codebook_size % 128 == 0 &&
+            c.n_ups >= 1 && c.n_ups <= 8 && c.n_res == 3 && c.gen_pre_k % 2 == 1 && c.gen_post_k % 2 == 1;
+  for (int i = 0; i < 4 && ok; ++i) ok = c.enc_dims[i] % 256 == 0 && c.enc_dims[i] <= 1024 && c.enc_depths[i] >= 0;
+  int ch = c.gen_channels;
+  for (int i = 0; i < c.n_ups && ok; ++i) {
+    ok = c.up_rates[i] >= 1 && c.up_rates[i] <= dcx::kMaxPhases && c.up_kernels[i] % c.up_rates[i] == 0 &&
+         (c.up_kernels[i] - c.up_rates[i]) % 2 == 0;
+    ch /= 2;
+    ok = ok && ch % 32 == 0;
+  }
+  ok = ok && (ch == 32 || ch == 64);
+  for (int i = 0; i < 3 && ok; ++i) ok = c.res_kernels[i] % 2 == 1;
+  if (!ok) return DCX_ERR_INVALID_ARG;
+  auto h = new (std::nothrow) dcx_codec();
+  if (!h) return DCX_ERR_OOM;
+  h->cfg = c;
+  hipGetDevice(&h->device);
+  *out = h;
+  return DCX_OK;
+}
+
+void dcx_destroy(dcx_codec* h) {
+  if (!h) return;
+  for (void* p : h->allocs) hipFree(p);
+  for (auto e : h->events) hipEventDestroy(e);
+  delete h;
+}
+
+int dcx_set_tensor(dcx_codec* h, const char* name, const float* data, int32_t ndim, const int64_t* shape) {
+  if (!h || !name || (!data && ndim > 0) || ndim < 0 || ndim > 8) return fail(h, DCX_ERR_INVALID_ARG, "bad tensor");
+  if (h->finalized) return fail(h, DCX_ERR_STATE, "dcx_set_tensor after dcx_finalize");
+  HostTensor t;
+  t.shape.assign(shape, shape + ndim);
+  const int64_t n = t.numel();
+  if (n < 0) return fail(h, DCX_ERR_INVALID_ARG, "negative shape");
+  t.data.assign(data, data + n);
+  h->host[name] = std::move(t);
+  return DCX_OK;
+}
+
+int dcx_finalize(dcx_codec* h, int32_t with_generator) {
+  if (!h) return DCX_ERR_INVALID_ARG;
+  if (h->finalized) return fail(h, DCX_ERR_STATE, "already finalized");
+  const dcx_config& c = h->cfg;
+  Builder B{h};
+  // ---- mel front end: DFT basis as a 4-tap conv over 256-sample rows ------------------
+  {
+    const int N = c.n_fft, nb = N / 2 + 1;
+    std::vector<double> win(N);
+    for (int n = 0; n < N; ++n) win[n] = 0.5 - 0.5 * std::cos(2.0 * M_PI * n / N);  // hann, periodic
+    std::vector<float> basis((size_t)N * N, 0.f);  // [col][n]; cols: re 0..512, im 1..511
+    for (int k = 0; k < nb; ++k)
+      for (int n = 0; n < N; ++n) {
+        const long long kn = ((long long)k * n) % N;
+        basis[(size_t)k * N + n] = (float)(win[n] * std::cos(2.0 * M_PI * kn / N));
+        if (k > 0 && k < nb - 1) basis[(size_t)(nb + k - 1) * N + n] = (float)(-win[n] * std::sin(2.0 * M_PI * kn / N));
+      }
+    h->dft.cin = c.hop; h->dft.cout = N; h->dft.taps = N / c.hop; h->dft.in_step = 1;
+    h->dft.w = B.upload(basis);
+    const int kpad = (nb + 15) / 16 * 16;
+    std::vector<double> fb = mel_fb(nb, c.f_min, c.f_max, c.n_mels, c.sample_rate);
+    std::vector<float> pk((size_t)c.n_mels * kpad, 0.f);
+    for (int m = 0; m < c.n_mels; ++m)
+      for (int k = 0; k < nb; ++k) pk[(size_t)m * kpad + k] = (float)fb[(size_t)k * c.n_mels + m];
+    h->melfb.cin = kpad; h->melfb.cout = c.n_mels; h->melfb.taps = 1;
+    h->melfb.w = B.upload(pk);
+  }
+  // ---- encoder --------------------------------------------------------------------------
+  {
+    const std::string e = "encoder.";
+    h->stem = B.conv(e + "downsample_layers.0.0", c.n_mels, c.enc_dims[0], 7, 1, 3);
+    h->stem_ln = B.ln(e + "downsample_layers.0.1", c.enc_dims[0]);
+    for (int i = 0; i < 4; ++i) {
+      if (i > 0) {
+        const std::string p = e + "downsample_layers." + std::to_string(i);
+        h->ds_ln[i] = B.ln(p + ".0", c.enc_dims[i - 1]);
+        h->ds_conv[i] = B.conv(p + ".1", c.enc_dims[i - 1], c.enc_dims[i], 1, 1, 0);
+      }
+      h->blocks[i].clear();
+      for (int j = 0; j < c.enc_depths[i]; ++j)
+        h->blocks[i].push_back(B.block(e + "stages." + std::to_string(i) + "." + std::to_string(j), c.enc_dims[i]));
+    }
+    h->enc_norm = B.ln(e + "norm", c.enc_dims[3]);
+  }
+  // ---- quantizer ------------------------------------------------------------------------
+  {
+    const std::string q = "quantizer.";
+    const int D = c.vq_dim, CD = c.codebook_dim, NC = c.codebook_size;
+    h->vq_down = B.conv(q + "downsample.0.0", D, D, 1, 1, 0);
+    h->vq_down_blk = B.block(q + "downsample.0.1", D);
+    h->vq_up = B.convT(q + "upsample.0.0", D, D, 1, 1);
+    h->vq_up_blk = B.block(q + "upsample.0.1", D);
+    h->vq_pin = B.conv(q + "grvq.rvqs.0.project_in", D, CD, 1, 1, 0);
+    ConvW pout = B.conv(q + "grvq.rvqs.0.project_out", CD, D, 1, 1, 0);
+    auto emb = B.need(q + "grvq.rvqs.0.layers.0._codebook.embed", {1, NC, CD});
+    if (emb) {
+      std::vector<float> e2(NC);
+      for (int i = 0; i < NC; ++i) {
+        double sacc = 0;
+        for (int d = 0; d < CD; ++d) sacc += (double)emb->data[(size_t)i * CD + d] * emb->data[(size_t)i * CD + d];
+        e2[i] = (float)sacc;
+      }
+      h->codebook = B.upload(emb->data);
+      h->e2 = B.upload(e2);
+    }
+    // decode table: project_out applied to every code once, E * W_out^T + b_out
+    h->ptable = B.alloc((size_t)NC * D);
+    if (!B.bad()) {
+      int rc = run_pointwise(h, pout, h->codebook, NC, h->ptable, 0);
+      if (rc != DCX_OK) return rc;
+      if (hipDeviceSynchronize() != hipSuccess) return fail(h, DCX_ERR_HIP, "decode-table build failed");
+    }
+  }
+  // ---- generator ------------------------------------------------------------------------
+  if (with_generator) {
+    const std::string g = "generator.";
+    int ch = c.gen_channels;
+    h->conv_pre = B.conv(g + "conv_pre", c.vq_dim, ch, c.gen_pre_k, 1, (c.gen_pre_k - 1) / 2);
+    for (int i = 0; i < c.n_ups; ++i) {
+      h->ups[i] = B.convT(g + "ups." + std::to_string(i), ch, ch / 2, c.up_kernels[i], c.up_rates[i]);
+      ch /= 2;
+      for (int rb = 0; rb < c.n_res; ++rb) {
+        const int k = c.res_kernels[rb];
+        for (int j = 0; j < 3; ++j) {
+          const int d = c.res_dilations[rb][j];
+          const std::string p = g + "resblocks." + std::to_string(i) + ".blocks." + std::to_string(rb);
+          h->res[i][rb][j][0] = B.conv(p + ".convs1." + std::to_string(j), ch, ch, k, d, (k * d - d) / 2);
+          h->res[i][rb][j][1] = B.conv(p + ".convs2." + std::to_string(j), ch, ch, k, 1, (k - 1) / 2);
+        }
+      }
+    }
+    HostTensor pw = B.weight(g + "conv_post", {1, ch, c.gen_post_k});
+    if (!B.bad()) {
+      std::vector<float> pk((size_t)c.gen_post_k * ch);
+      for (int i = 0; i < ch; ++i)
+        for (int j = 0; j < c.gen_post_k; ++j) pk[(size_t)j * ch + i] = pw.data[(size_t)i * c.gen_post_k + j];
+      h->post_w = B.upload(pk);
+      auto pb = B.need(g + "conv_post.bias", {1});
+      if (pb) h->post_b = pb->data[0];
+    }
+  }
+  if (B.bad()) return fail(h, B.e.code, B.e.msg);
+  h->has_gen = with_generator != 0;
+  h->finalized = true;
+  h->host.clear();
+  return DCX_OK;
+}
+
+int64_t dcx_num_frames(const dcx_codec* h, int64_t n) { return h ? frames_of(h->cfg, n) : 0; }
+
+size_t dcx_workspace_size(const dcx_codec* h, int32_t batch, int64_t frames) {
+  if (!h || batch <= 0 || frames <= 0) return 0;
+  dcx_codec* hh = const_cast<dcx_codec*>(h);
+  const int64_t n = (frames - 1) * h->cfg.hop + h->cfg.n_fft - (h->cfg.win - h->cfg.hop);
+  Bump d(nullptr, 0, true);
+  stage_encode_decode(hh, nullptr, batch, n, nullptr, nullptr, d, 0);
+  size_t need = d.off;
+  Bump q(nullptr, 0, true);  // vq_encode with every optional output in the workspace
+  stage_vq_encode(hh, nullptr, batch, (int)frames, nullptr, nullptr, nullptr, nullptr, q, 0);
+  need = std::max(need, q.off + (size_t)batch * frames * (h->cfg.codebook_dim + h->cfg.vq_dim) * 4 + 1024);
+  return need + 4096;
+}
+
+#define STAGE_PRE(need_gen)                                           \
+  int rc_ = check_ready(h, need_gen);                                 \
+  if (rc_ != DCX_OK) return rc_;                                      \
+  if (batch <= 0) return fail(h, DCX_ERR_INVALID_ARG, "batch must be > 0"); \
+  hipStream_t s = (hipStream_t)stream;                                \
+  Bump ws(workspace, ws_bytes, false)
+
+int dcx_mel(dcx_codec* h, const float* audio, int32_t batch, int64_t n, float* mel, void* workspace, size_t ws_bytes,
+            void* stream) {
+  STAGE_PRE(false);
+  if (!audio || !mel) return fail(h, DCX_ERR_INVALID_ARG, "null buffer");
+  if (n <= (h->cfg.win - h->cfg.hop) / 2 || frames_of(h->cfg, n) < 1)
+    return fail(h, DCX_ERR_INVALID_ARG, "clip too short for the reflect pad / one STFT frame");
+  return stage_mel(h, audio, batch, n, mel, ws, s);
+}
+
+int dcx_encode(dcx_codec* h, const float* mel, int32_t batch, int64_t frames, float* feat, void* workspace,
+               size_t ws_bytes, void* stream) {
+  STAGE_PRE(false);
+  if (!mel || !feat || frames <= 0) return fail(h, DCX_ERR_INVALID_ARG, "bad arguments");
+  return stage_encode(h, mel, batch, (int)frames, feat, ws, s);
+}
+
+int dcx_vq_encode(dcx_codec* h, const float* feat, int32_t batch, int64_t frames, int32_t* codes, float* x_pjt_in,
+                  float* quantized_fup, float* quantized, void* workspace, size_t ws_bytes, void* stream) {
+  STAGE_PRE(false);
+  if (!feat || !codes || frames <= 0) return fail(h, DCX_ERR_INVALID_ARG, "bad arguments");
+  return stage_vq_encode(h, feat, batch, (int)frames, codes, x_pjt_in, quantized_fup, quantized, ws, s);
+}
+
+int dcx_vq_decode(dcx_codec* h, const int32_t* codes, int32_t batch, int64_t frames, float* z, int32_t* n_invalid,
+                  void* workspace, size_t ws_bytes, void* stream) {
+  STAGE_PRE(false);
+  if (!codes || !z || frames <= 0) return fail(h, DCX_ERR_INVALID_ARG, "bad arguments");
+  return stage_vq_decode(h, codes, batch, (int)frames, z, n_invalid, ws, s);
+}
+
+int dcx_generate(dcx_codec* h, const float* z, int32_t batch, int64_t frames, float* wav, void* workspace,
+                 size_t ws_bytes, void* stream) {
+  STAGE_PRE(true);
+  if (!z || !wav || frames <= 0) return fail(h, DCX_ERR_INVALID_ARG, "bad arguments");
+  return stage_generate(h, z, batch, (int)frames, wav, ws, s);
+}
+
+int dcx_encode_decode(dcx_codec* h, const float* audio, int32_t batch, int64_t n, int32_t* codes, float* wav,
+                      void* workspace, size_t ws_bytes, void* stream) {
+  STAGE_PRE(true);
+  if (!audio || !codes || !wav) return fail(h, DCX_ERR_INVALID_ARG, "null buffer");
+  if (n <= (h->cfg.win - h->cfg.hop) / 2 || frames_of(h->cfg, n) < 1)
+    return fail(h, DCX_ERR_INVALID_ARG, "clip too short for the reflect pad / one STFT frame");
+  return stage_encode_decode(h, audio, batch, n, codes, wav, ws, s);
+}
+
+int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int64_t cols, void* stream) {
+  if (!in || !out || batch <= 0 || rows <= 0 || cols <= 0) return DCX_ERR_INVALID_ARG;
+  return dcx::launch_transpose(in, out, batch, rows, cols, (hipStream_t)stream) == hipSuccess ? DCX_OK : DCX_ERR_HIP;
+}
+
+int dcx_profile_enable(dcx_codec* h, int32_t on) {
+  if (!h) return DCX_ERR_INVALID_ARG;
+  h->prof = on != 0;
+  return DCX_OK;
+}
+
+int dcx_profile_reset(dcx_codec* h) {
+  if (!h) return DCX_ERR_INVALID_ARG;
+  prof_collect(h);
+  for (size_t i = 0; i < h->prof_names.size(); ++i) {
+    h->prof_launches[i] = 0;
+    h->prof_ms[i] = h->prof_flops[i] = h->prof_bytes[i] = 0;
+  }
+  return DCX_OK;
+}
+
+int32_t dcx_profile_count(const dcx_codec* h) { return h ? (int32_t)h->prof_names.size() : 0; }
+
+int dcx_profile_read(dcx_codec* h, int32_t i, const char** name, int64_t* launches, double* ms, double* flops,
+                     double* bytes) {
+  if (!h) return DCX_ERR_INVALID_ARG;
+  prof_collect(h);
+  if (i < 0 || i >= (int32_t)h->prof_names.size()) return DCX_ERR_INVALID_ARG;
+  if (name) *name = h->prof_names[i].c_str();
+  if (launches) *launches = h->prof_launches[i];
+  if (ms) *ms = h->prof_ms[i];
+  if (flops) *flops = h->prof_flops[i];
+  if (bytes) *bytes = h->prof_bytes[i];
+  return DCX_OK;
+}
+
+}  // extern "C"

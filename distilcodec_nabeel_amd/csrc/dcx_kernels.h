@@ -1,0 +1,69 @@
+// Internal interface between the host orchestration (dcx_api.cpp) and the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dcx {
+
+// Epilogue of the implicit-GEMM convolution (applied per output element v = acc + bias).
+enum Epi : int {
+  EPI_BIAS = 0,       // v
+  EPI_GELU = 1,       // gelu_erf(v)                     ConvNeXt pwconv1 + nn.GELU()
+  EPI_GAMMA_RES = 2,  // res + gamma * v                 ConvNeXt pwconv2, layer scale, residual
+  EPI_RES = 3,        // res + v                         ResBlock1 `x = xt + x`
+  EPI_LOGCLAMP = 4,   // log(max(v, 1e-5))               LogMelSpectrogram.compress
+};
+
+// ParallelBlock mean of the 3 ResBlock1 outputs (convnext_utils.py:137-138), folded into the
+// epilogue of each ResBlock's last conv: first writes, mid adds, last adds and divides by 3.
+enum Mean : int { MEAN_NONE = 0, MEAN_FIRST = 1, MEAN_MID = 2, MEAN_LAST = 3 };
+
+constexpr int kMaxPhases = 8;
+
+// out[b][q*out_mul + phase][co] = epi( sum_{m<taps} sum_{ci<Cin} x[b][q + in_base[phase] + m*in_step][ci]
+//                                       * w[phase][co][m*Cin + ci] + bias[co] )
+// Rows of x outside [0, Lin) read as zero (zero padding).  Channels-last everywhere.
+struct ConvParams {
+  const float* x;
+  const float* w;
+  const float* bias;   // may be null
+  const float* gamma;  // EPI_GAMMA_RES
+  const float* res;    // EPI_GAMMA_RES / EPI_RES, layout of y
+  float* y;            // v (may be null)
+  float* y2;           // silu(v) (may be null)
+  float* macc;         // mean accumulator, layout of y (MEAN_* != NONE)
+  long long x_bstride;      // elements between clips in x
+  long long y_bstride;      // elements between clips in y / y2 / res / macc
+  long long w_phase_stride; // elements between phases in w
+  int Lin, Lq, Cin, Cout, ldx, ldy;
+  int taps, in_step, out_mul;
+  int in_base[kMaxPhases];
+  int epi, mean_mode;
+  // argmin epilogue (VQ search)
+  const float* x2;      // [rows] squared norms of x rows
+  const float* e2;      // [Cout] squared norms of the codebook rows
+  float* part_val;      // [rows][ntiles]
+  int* part_idx;        // [rows][ntiles]
+};
+
+// Launchers (all stream-ordered, no allocation).  Return hipError_t of the launch.
+hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname);
+hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname);
+int vq_argmin_ntiles(int ncodes);
+hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows, int ntiles, int32_t* codes,
+                            hipStream_t s);
+hipError_t launch_row_sqnorm(const float* x, long long rows, int C, float* out, hipStream_t s);
+hipError_t launch_ln_rows(const float* x, float* y, const float* w, const float* b, long long rows, int C, float eps,
+                          int channels_first_form, hipStream_t s);
+hipError_t launch_dwconv_ln(const float* x, float* y, const float* dww, const float* dwb, const float* lnw,
+                            const float* lnb, int batch, int L, int C, hipStream_t s);
+hipError_t launch_frame_pad(const float* audio, float* frames, int batch, long long n, int rows, int hop, int pad_left,
+                            hipStream_t s);
+hipError_t launch_spec_mag(const float* spec, float* mag, long long rows, int nbins, int ld_out, hipStream_t s);
+hipError_t launch_gather_rows(const float* table, int ntable, const int32_t* idx, long long rows, int width,
+                              float* out, int32_t* n_invalid, hipStream_t s);
+hipError_t launch_conv_post_tanh(const float* x, const float* w, float bias, float* out, int batch, int L, int C,
+                                 int k, hipStream_t s);
+hipError_t launch_transpose(const float* in, float* out, int batch, long long rows, long long cols, hipStream_t s);
+
+}  // namespace dcx

@@ -1,0 +1,342 @@
+// Bandwidth-bound kernels of the DistilCodec path (gfx950): row LayerNorms, the fused
+// depthwise-conv + LayerNorm front of each ConvNeXt block, the STFT framing / magnitude steps,
+// codebook gathers, the VQ partial-argmin reduction, conv_post + tanh, and a batched transpose.
+// All use 16-byte accesses along the contiguous channel axis (channels-last layout).
+#include "dcx_kernels.h"
+
+namespace dcx {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// LayerNorm over the channel axis of each row.  channels_first_form=1 follows the reference's
+// custom channels_first LayerNorm `(x-u)/sqrt(s+eps)*w+b` (convnext_utils.py:208-213);
+// 0 follows F.layer_norm (`(x-u)*rsqrt(s+eps)*w+b`, convnext_utils.py:205).  Biased variance.
+// One wave per row, NV float4 per lane (C = 256*NV).
+// ---------------------------------------------------------------------------------------------
+template <int NV>
+__device__ __forceinline__ void ln_finish(f32x4 (&v)[NV], int C, float eps, int cf, const float* __restrict__ w,
+                                          const float* __restrict__ b, float* __restrict__ yrow, int lane) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  const float mean = wave_sum(s) / (float)C;
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const f32x4 d = v[i] - mean;
+    sq += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+  }
+  const float var = wave_sum(sq) / (float)C;
+  const float den = sqrtf(var + eps);
+  const float rstd = 1.0f / den;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(w + c);
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(b + c);
+    f32x4 o;
+    if (cf) {
+      o = (v[i] - mean) / den * wv + bv;
+    } else {
+      o = (v[i] - mean) * rstd * wv + bv;
+    }
+    *reinterpret_cast<f32x4*>(yrow + c) = o;
+  }
+}
+
+template <int NV>
+__global__ void __launch_bounds__(256) ln_rows_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                       const float* __restrict__ w, const float* __restrict__ b,
+                                                       long long rows, float eps, int cf) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int C = 256 * NV;
+  f32x4 v[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = *reinterpret_cast<const f32x4*>(x + row * C + (lane + 64 * i) * 4);
+  ln_finish<NV>(v, C, eps, cf, w, b, y + row * C, lane);
+}
+
+hipError_t launch_ln_rows(const float* x, float* y, const float* w, const float* b, long long rows, int C, float eps,
+                          int cf, hipStream_t s) {
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  switch (C) {
+    case 256: hipLaunchKernelGGL(ln_rows_kernel<1>, grid, block, 0, s, x, y, w, b, rows, eps, cf); break;
+    case 512: hipLaunchKernelGGL(ln_rows_kernel<2>, grid, block, 0, s, x, y, w, b, rows, eps, cf); break;
+    case 768: hipLaunchKernelGGL(ln_rows_kernel<3>, grid, block, 0, s, x, y, w, b, rows, eps, cf); break;
+    case 1024: hipLaunchKernelGGL(ln_rows_kernel<4>, grid, block, 0, s, x, y, w, b, rows, eps, cf); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ConvNeXtBlock front (convnext_utils.py:266-268): depthwise Conv1d k7 p3 (+bias) then
+// F.layer_norm over channels.  dww is packed [7][C].  One wave per output row.
+template <int NV>
+__global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                         const float* __restrict__ dww, const float* __restrict__ dwb,
+                                                         const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                                         int L, long long rows) {
+  constexpr int C = 256 * NV;
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const long long bidx = row / L;
+  const int t = (int)(row - bidx * L);
+  const float* xb = x + bidx * (long long)L * C;
+  f32x4 v[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int tt = t + j - 3;
+      if (tt >= 0 && tt < L) {
+        const f32x4 xv = *reinterpret_cast<const f32x4*>(xb + (long long)tt * C + c);
+        const f32x4 wv = *reinterpret_cast<const f32x4*>(dww + j * C + c);
+        acc += xv * wv;
+      }
+    }
+    v[i] = acc + *reinterpret_cast<const f32x4*>(dwb + c);
+  }
+  ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y + row * C, lane);
+}
+
+hipError_t launch_dwconv_ln(const float* x, float* y, const float* dww, const float* dwb, const float* lnw,
+                            const float* lnb, int batch, int L, int C, hipStream_t s) {
+  const long long rows = (long long)batch * L;
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  switch (C) {
+    case 256: hipLaunchKernelGGL(dwconv_ln_kernel<1>, grid, block, 0, s, x, y, dww, dwb, lnw, lnb, L, rows); break;
+    case 512: hipLaunchKernelGGL(dwconv_ln_kernel<2>, grid, block, 0, s, x, y, dww, dwb, lnw, lnb, L, rows); break;
+    case 768: hipLaunchKernelGGL(dwconv_ln_kernel<3>, grid, block, 0, s, x, y, dww, dwb, lnw, lnb, L, rows); break;
+    case 1024: hipLaunchKernelGGL(dwconv_ln_kernel<4>, grid, block, 0, s, x, y, dww, dwb, lnw, lnb, L, rows); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// STFT framing: reflect pad ((win-hop)/2 each side, mel_spec.py:30-37) and cut the padded
+// signal into rows of `hop` samples, so frame f = rows f..f+3 (a 4-tap conv over 256 channels).
+// ---------------------------------------------------------------------------------------------
+__global__ void frame_pad_kernel(const float* __restrict__ audio, float* __restrict__ frames, long long n, int rows,
+                                 int hop, int pad_left) {
+  const int b = blockIdx.y;
+  const long long total = (long long)rows * hop;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    long long src = i - pad_left;
+    if (src < 0) src = -src;
+    if (src >= n) src = 2 * (n - 1) - src;
+    frames[(long long)b * total + i] = audio[(long long)b * n + src];
+  }
+}
+
+hipError_t launch_frame_pad(const float* audio, float* frames, int batch, long long n, int rows, int hop, int pad_left,
+                            hipStream_t s) {
+  const long long total = (long long)rows * hop;
+  unsigned gx = (unsigned)((total + 255) / 256);
+  if (gx > 4096) gx = 4096;
+  hipLaunchKernelGGL(frame_pad_kernel, dim3(gx, batch), dim3(256), 0, s, audio, frames, n, rows, hop, pad_left);
+  return hipGetLastError();
+}
+
+// |STFT| = sqrt(re^2 + im^2 + 1e-6) (mel_spec.py:54-55).  spec columns: [0, nbins) real part of
+// bins 0..nbins-1, [nbins, 2*nbins-2) imaginary part of bins 1..nbins-2 (bins 0 and n_fft/2 are
+// real for a real signal).  Output row padded with zeros to ld_out.
+__global__ void spec_mag_kernel(const float* __restrict__ spec, float* __restrict__ mag, long long rows, int nbins,
+                                int ld_out) {
+  const long long row = blockIdx.x;
+  if (row >= rows) return;
+  const int ld_in = 2 * nbins - 2;
+  for (int k = threadIdx.x; k < ld_out; k += blockDim.x) {
+    float o = 0.f;
+    if (k < nbins) {
+      const float re = spec[row * ld_in + k];
+      const float im = (k > 0 && k < nbins - 1) ? spec[row * ld_in + nbins + k - 1] : 0.f;
+      o = sqrtf((re * re + im * im) + 1e-6f);
+    }
+    mag[row * ld_out + k] = o;
+  }
+}
+
+hipError_t launch_spec_mag(const float* spec, float* mag, long long rows, int nbins, int ld_out, hipStream_t s) {
+  hipLaunchKernelGGL(spec_mag_kernel, dim3((unsigned)rows), dim3(256), 0, s, spec, mag, rows, nbins, ld_out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// VQ helpers
+// ---------------------------------------------------------------------------------------------
+// |x|^2 per row (vector_quantize_pytorch.py:42), accumulated in fp64 and rounded once.
+__global__ void __launch_bounds__(256) row_sqnorm_kernel(const float* __restrict__ x, long long rows, int C,
+                                                          float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  double s = 0.0;
+  for (int c = lane * 4; c < C; c += 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + row * C + c);
+    s += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) out[row] = (float)s;
+}
+
+hipError_t launch_row_sqnorm(const float* x, long long rows, int C, float* out, hipStream_t s) {
+  if (C % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(row_sqnorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, rows, C, out);
+  return hipGetLastError();
+}
+
+// Combine per-tile (distance, index) partials: smallest distance, lowest index on ties.
+__global__ void vq_reduce_kernel(const float* __restrict__ pv, const int* __restrict__ pi, int rows, int ntiles,
+                                 int32_t* __restrict__ codes) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float bv = __builtin_inff();
+  int bi = 0x7fffffff;
+  for (int t = lane; t < ntiles; t += 64) {
+    const float v = pv[(long long)row * ntiles + t];
+    const int i = pi[(long long)row * ntiles + t];
+    if (v < bv || (v == bv && i < bi)) { bv = v; bi = i; }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float ov = __shfl_xor(bv, off, 64);
+    const int oi = __shfl_xor(bi, off, 64);
+    if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  }
+  if (lane == 0) codes[row] = bi;
+}
+
+hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows, int ntiles, int32_t* codes,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(vq_reduce_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, part_val, part_idx, rows,
+                     ntiles, codes);
+  return hipGetLastError();
+}
+
+// out[r] = table[idx[r]] (batched_embedding / einx.get_at).  Negative indices wrap like torch
+// indexing; anything still outside [0, ntable) reads row 0 and is counted.
+__global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restrict__ table, int ntable,
+                                                           const int32_t* __restrict__ idx, long long rows, int width,
+                                                           float* __restrict__ out, int32_t* n_invalid) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  int i = idx[row];
+  if (i < 0) i += ntable;
+  if (i < 0 || i >= ntable) {
+    if (lane == 0 && n_invalid) atomicAdd(n_invalid, 1);
+    i = 0;
+  }
+  const float* src = table + (long long)i * width;
+  float* dst = out + row * width;
+  for (int c = lane * 4; c < width; c += 256)
+    *reinterpret_cast<f32x4*>(dst + c) = *reinterpret_cast<const f32x4*>(src + c);
+}
+
+hipError_t launch_gather_rows(const float* table, int ntable, const int32_t* idx, long long rows, int width, float* out,
+                              int32_t* n_invalid, hipStream_t s) {
+  if (width % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, table, ntable, idx, rows,
+                     width, out, n_invalid);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// conv_post (C -> 1, kernel k, "same" padding) + tanh (generators.py:141-145).  The input is
+// already silu-activated by the previous stage's epilogue.  Block = 256 output samples; the
+// input rows they touch are staged once in LDS (row stride 36 floats: conflict-free b128 reads).
+// ---------------------------------------------------------------------------------------------
+template <int C>
+__global__ void __launch_bounds__(256) conv_post_tanh_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                              float bias, float* __restrict__ out, int L, int k) {
+  constexpr int LD = C + 4;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int pad = (k - 1) / 2;
+  const int rows = 256 + k - 1;
+  float* tile = sm;                 // [rows][LD]
+  float* ws = sm + rows * LD;       // [k][C]
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * 256;
+  const float* xb = x + (long long)b * L * C;
+  for (int i = threadIdx.x; i < rows * (C / 4); i += 256) {
+    const int r = i / (C / 4), c4 = i % (C / 4);
+    const int t = t0 - pad + r;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (t >= 0 && t < L) v = *reinterpret_cast<const f32x4*>(xb + (long long)t * C + c4 * 4);
+    *reinterpret_cast<f32x4*>(tile + r * LD + c4 * 4) = v;
+  }
+  for (int i = threadIdx.x; i < k * C; i += 256) ws[i] = w[i];
+  __syncthreads();
+  const int t = t0 + threadIdx.x;
+  if (t >= L) return;
+  float acc = 0.f;
+  for (int j = 0; j < k; ++j) {
+    const float* xr = tile + (threadIdx.x + j) * LD;
+    const float* wr = ws + j * C;
+#pragma unroll
+    for (int c = 0; c < C; c += 4) {
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(xr + c);
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(wr + c);
+      acc = fmaf(xv.x, wv.x, acc);
+      acc = fmaf(xv.y, wv.y, acc);
+      acc = fmaf(xv.z, wv.z, acc);
+      acc = fmaf(xv.w, wv.w, acc);
+    }
+  }
+  out[(long long)b * L + t] = tanhf(acc + bias);
+}
+
+hipError_t launch_conv_post_tanh(const float* x, const float* w, float bias, float* out, int batch, int L, int C, int k,
+                                 hipStream_t s) {
+  dim3 grid((unsigned)((L + 255) / 256), batch);
+  const size_t lds = (size_t)((256 + k - 1) * (C + 4) + k * C) * sizeof(float);
+  switch (C) {
+    case 32: hipLaunchKernelGGL(conv_post_tanh_kernel<32>, grid, dim3(256), lds, s, x, w, bias, out, L, k); break;
+    case 64: hipLaunchKernelGGL(conv_post_tanh_kernel<64>, grid, dim3(256), lds, s, x, w, bias, out, L, k); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// [B][R][C] -> [B][C][R] through a 32x33 LDS tile.
+// ---------------------------------------------------------------------------------------------
+__global__ void transpose_kernel(const float* __restrict__ in, float* __restrict__ out, long long R, long long C) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z;
+  const long long r0 = (long long)blockIdx.y * 32, c0 = (long long)blockIdx.x * 32;
+  const float* ib = in + (long long)b * R * C;
+  float* ob = out + (long long)b * R * C;
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    const long long r = r0 + i, c = c0 + threadIdx.x;
+    if (r < R && c < C) tile[i][threadIdx.x] = ib[r * C + c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    const long long c = c0 + i, r = r0 + threadIdx.x;
+    if (r < R && c < C) ob[c * R + r] = tile[threadIdx.x][i];
+  }
+}
+
+hipError_t launch_transpose(const float* in, float* out, int batch, long long rows, long long cols, hipStream_t s) {
+  dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32), batch);
+  hipLaunchKernelGGL(transpose_kernel, grid, dim3(32, 8), 0, s, in, out, rows, cols);
+  return hipGetLastError();
+}
+
+}  // namespace dcx

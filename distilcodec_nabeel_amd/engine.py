@@ -1,0 +1,191 @@
+"""Device-side engine: one libdcx handle per GPU, torch tensors as device buffers.
+
+Every method is stream-ordered on `torch.cuda.current_stream(device)` and hands raw device
+pointers to the C ABI.  Tensors are channels-last ([B][T][C]) as the kernels produce them.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native
+from .config import check_supported
+
+
+class NativeCodec:
+    def __init__(self, cfg: dict, state: dict, device, with_generator: bool = True):
+        check_supported(cfg)
+        self.cfg = cfg
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise _native.NativeUnavailable("the DistilCodec MI355X path needs a GPU device (cuda:N on ROCm)")
+        if not torch.cuda.is_available():
+            raise _native.NativeUnavailable("no GPU visible to torch: the HIP path cannot run here")
+        self.L = _native.lib()
+        self.c = _native.config_from_dict(cfg)
+        self.D = cfg["quantizer"]["input_dim"]
+        self.CD = cfg["quantizer"]["codebook_dim"]
+        self.NC = cfg["quantizer"]["codebook_size"]
+        self.n_mels = cfg["spec_transform"]["num_mels"]
+        self.hop = cfg["spec_transform"]["hop_size"]
+        self.with_generator = with_generator
+        self._ws = None
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            self._check(self.L.dcx_create(ctypes.byref(self.c), ctypes.byref(h)), None)
+            self.h = h
+            for part in ("encoder", "quantizer") + (("generator",) if with_generator else ()):
+                for k, v in state[part].items():
+                    a = np.ascontiguousarray(np.asarray(v, dtype=np.float32))
+                    shape = (ctypes.c_int64 * max(a.ndim, 1))(*a.shape)
+                    self._check(self.L.dcx_set_tensor(self.h, f"{part}.{k}".encode(), a.ctypes.data_as(ctypes.c_void_p),
+                                                      a.ndim, shape))
+            self._check(self.L.dcx_finalize(self.h, 1 if with_generator else 0))
+
+    # ------------------------------------------------------------------ plumbing
+    def _check(self, rc, h="self"):
+        if rc == _native.DCX_OK:
+            return
+        msg = ""
+        handle = self.h if h == "self" else h
+        if handle:
+            msg = self.L.dcx_last_error(handle).decode()
+        msg = msg or self.L.dcx_status_string(rc).decode()
+        if rc == _native.DCX_ERR_INVALID_ARG:
+            raise ValueError(msg)
+        if rc == _native.DCX_ERR_MISSING_WEIGHT:
+            raise KeyError(msg)
+        raise _native.NativeError(rc, msg)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            try:
+                self.L.dcx_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def workspace(self, batch: int, frames: int) -> torch.Tensor:
+        need = int(self.L.dcx_workspace_size(self.h, batch, frames))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = None
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    @staticmethod
+    def _ptr(t):
+        return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+    def _dev(self, t, dtype):
+        t = torch.as_tensor(t)
+        if t.device != self.device or t.dtype != dtype or not t.is_contiguous():
+            t = t.to(device=self.device, dtype=dtype).contiguous()
+        return t
+
+    def num_frames(self, n_samples: int) -> int:
+        return int(self.L.dcx_num_frames(self.h, n_samples))
+
+    # ------------------------------------------------------------------ stages
+    def mel(self, audio: torch.Tensor) -> torch.Tensor:
+        """audio (B, N) fp32 (with the reference's leading zero) -> mel (B, T, n_mels)."""
+        audio = self._dev(audio, torch.float32)
+        B, N = audio.shape
+        T = self.num_frames(N)
+        out = torch.empty(B, T, self.n_mels, device=self.device)
+        ws = self.workspace(B, T)
+        with torch.cuda.device(self.device):
+            self._check(self.L.dcx_mel(self.h, self._ptr(audio), B, N, self._ptr(out), self._ptr(ws), ws.numel(), self._stream()))
+        return out
+
+    def encode(self, mel: torch.Tensor) -> torch.Tensor:
+        mel = self._dev(mel, torch.float32)
+        B, T, _ = mel.shape
+        out = torch.empty(B, T, self.cfg["encoder"]["dims"][-1], device=self.device)
+        ws = self.workspace(B, T)
+        with torch.cuda.device(self.device):
+            self._check(self.L.dcx_encode(self.h, self._ptr(mel), B, T, self._ptr(out), self._ptr(ws), ws.numel(), self._stream()))
+        return out
+
+    def vq_encode(self, feat: torch.Tensor, want_pjt_in=True, want_fup=True, want_quantized=True):
+        feat = self._dev(feat, torch.float32)
+        B, T, _ = feat.shape
+        codes = torch.empty(B, T, dtype=torch.int32, device=self.device)
+        pin = torch.empty(B, T, self.CD, device=self.device) if want_pjt_in else None
+        fup = torch.empty(B, T, self.CD, device=self.device) if want_fup else None
+        q = torch.empty(B, T, self.D, device=self.device) if want_quantized else None
+        ws = self.workspace(B, T)
+        with torch.cuda.device(self.device):
+            self._check(self.L.dcx_vq_encode(self.h, self._ptr(feat), B, T, self._ptr(codes), self._ptr(pin), self._ptr(fup),
+                                             self._ptr(q), self._ptr(ws), ws.numel(), self._stream()))
+        return codes, pin, fup, q
+
+    def vq_decode(self, codes: torch.Tensor) -> torch.Tensor:
+        codes = self._dev(codes, torch.int32)
+        B, T = codes.shape
+        z = torch.empty(B, T, self.D, device=self.device)
+        ws = self.workspace(B, T)
+        with torch.cuda.device(self.device):
+            self._check(self.L.dcx_vq_decode(self.h, self._ptr(codes), B, T, self._ptr(z), None, self._ptr(ws), ws.numel(),
+                                             self._stream()))
+        return z
+
+    def generate(self, z: torch.Tensor) -> torch.Tensor:
+        if not self.with_generator:
+            raise RuntimeError("this engine was built without generator weights")
+        z = self._dev(z, torch.float32)
+        B, T, _ = z.shape
+        wav = torch.empty(B, self.hop * T, device=self.device)
+        ws = self.workspace(B, T)
+        with torch.cuda.device(self.device):
+            self._check(self.L.dcx_generate(self.h, self._ptr(z), B, T, self._ptr(wav), self._ptr(ws), ws.numel(), self._stream()))
+        return wav
+
+    def encode_decode(self, audio: torch.Tensor, codes: torch.Tensor | None = None, wav: torch.Tensor | None = None):
+        audio = self._dev(audio, torch.float32)
+        B, N = audio.shape
+        T = self.num_frames(N)
+        if codes is None:
+            codes = torch.empty(B, T, dtype=torch.int32, device=self.device)
+        if wav is None:
+            wav = torch.empty(B, self.hop * T, device=self.device)
+        ws = self.workspace(B, T)
+        with torch.cuda.device(self.device):
+            self._check(self.L.dcx_encode_decode(self.h, self._ptr(audio), B, N, self._ptr(codes), self._ptr(wav), self._ptr(ws),
+                                                 ws.numel(), self._stream()))
+        return codes, wav
+
+    def transpose(self, x: torch.Tensor) -> torch.Tensor:
+        """(B, R, C) -> (B, C, R) contiguous, on device, by the HIP transpose kernel."""
+        x = self._dev(x, torch.float32)
+        B, R, C = x.shape
+        out = torch.empty(B, C, R, device=self.device)
+        with torch.cuda.device(self.device):
+            rc = self.L.dcx_transpose(self._ptr(x), self._ptr(out), B, R, C, self._stream())
+        if rc != _native.DCX_OK:
+            raise _native.NativeError(rc, "dcx_transpose failed")
+        return out
+
+    # ------------------------------------------------------------------ profiling
+    def profile(self, on: bool):
+        self._check(self.L.dcx_profile_enable(self.h, 1 if on else 0))
+
+    def profile_reset(self):
+        self._check(self.L.dcx_profile_reset(self.h))
+
+    def profile_read(self) -> dict:
+        out = {}
+        n = self.L.dcx_profile_count(self.h)
+        for i in range(n):
+            name = ctypes.c_char_p()
+            launches = ctypes.c_int64()
+            ms, fl, by = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+            self._check(self.L.dcx_profile_read(self.h, i, ctypes.byref(name), ctypes.byref(launches), ctypes.byref(ms),
+                                                ctypes.byref(fl), ctypes.byref(by)))
+            out[name.value.decode()] = {"launches": launches.value, "ms": ms.value, "flops": fl.value, "bytes": by.value}
+        return out

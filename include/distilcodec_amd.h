@@ -1,0 +1,141 @@
+/*
+ * distilcodec_amd.h -- C ABI of the MI355X-native DistilCodec encode -> quantize -> decode path.
+ *
+ * The reference (nabeelscicom/DistilCodec_nabeel, pure Python/PyTorch) has no native interface;
+ * this ABI replaces the PyTorch library kernels under the reference's own Python surface
+ * (`distilcodec.DistilCodec`, distilcodec/distil_codec.py).  Each entry point below names the
+ * reference code it replaces (paths relative to the reference checkout).
+ *
+ * Conventions
+ *  - One handle = one device (the HIP device current when dcx_create is called).
+ *  - Feature tensors are channels-last fp32: [B][T][C] (T = frames, 93.75 frames/s at 24 kHz).
+ *    The Python shim exposes the reference's channels-first (B, C, T) views on top.
+ *  - Every stage call is stream-ordered on the given hipStream_t (passed as void*), allocates
+ *    nothing, never synchronises the host, and is therefore hipGraph-capturable.  Device
+ *    buffers (inputs, outputs, workspace) are owned by the caller.
+ *  - Return value: DCX_OK (0) or a negative DCX_ERR_* status; dcx_last_error() has the text.
+ *    No C++ exception crosses the ABI.  A handle is not re-entrant: callers serialise per handle.
+ */
+#ifndef DISTILCODEC_AMD_H
+#define DISTILCODEC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCX_ABI_VERSION 1
+
+enum {
+  DCX_OK = 0,
+  DCX_ERR_INVALID_ARG = -1,    /* bad shape / null pointer / unsupported config value */
+  DCX_ERR_MISSING_WEIGHT = -2, /* dcx_finalize: a required checkpoint tensor was never set */
+  DCX_ERR_STATE = -3,          /* call order violated (e.g. stage call before dcx_finalize) */
+  DCX_ERR_HIP = -4,            /* a HIP runtime call failed */
+  DCX_ERR_OOM = -5,            /* device allocation failed (dcx_finalize only) */
+  DCX_ERR_WORKSPACE = -6       /* workspace smaller than dcx_workspace_size() */
+};
+
+typedef struct dcx_codec dcx_codec;
+
+/* Geometry of the model; mirrors configs/model_config.json (DistilCodec.__init__,
+ * distilcodec/distil_codec.py:30-70).  Only the published geometry family is supported
+ * (G=1, R=1, downsample factor 1, no template branch); others return DCX_ERR_INVALID_ARG. */
+typedef struct dcx_config {
+  int32_t sample_rate;          /* 24000 */
+  int32_t n_fft, hop, win;      /* 1024, 256, 1024 (mel_spec.py) */
+  int32_t n_mels;               /* 128 */
+  float f_min, f_max;           /* 0, 12000 */
+  int32_t enc_depths[4];        /* 3,3,9,3 (encoders.py:21-60) */
+  int32_t enc_dims[4];          /* 256,512,768,1024 */
+  int32_t vq_dim;               /* 1024 (grfvq.py input_dim) */
+  int32_t codebook_dim;         /* 3584 */
+  int32_t codebook_size;        /* 32768 */
+  int32_t gen_channels;         /* 1024 (upsample_initial_channel) */
+  int32_t gen_pre_k, gen_post_k;/* 13, 13 */
+  int32_t n_ups;                /* 5 */
+  int32_t up_rates[8];          /* 8,4,2,2,2 */
+  int32_t up_kernels[8];        /* 16,12,4,4,4 */
+  int32_t n_res;                /* 3 */
+  int32_t res_kernels[4];       /* 3,7,11 */
+  int32_t res_dilations[4][4];  /* {1,3,5} x3 */
+} dcx_config;
+
+/* Fills the published DistilCodec 24 kHz geometry. */
+void dcx_default_config(dcx_config* cfg);
+
+/* Create a handle on the current HIP device.  Replaces DistilCodec.__init__ (:30-70). */
+int dcx_create(const dcx_config* cfg, dcx_codec** out);
+void dcx_destroy(dcx_codec* h);
+const char* dcx_last_error(const dcx_codec* h);
+const char* dcx_status_string(int status);
+int dcx_abi_version(void);
+
+/* Checkpoint ingestion (replaces load_state_dict in DistilCodec.from_pretrained, :77-97).
+ * `name` is "<part>.<state-dict key>" with part in {encoder, quantizer, generator}, e.g.
+ * "generator.ups.0.parametrizations.weight.original1".  Weight-norm pairs (original0/1 or
+ * weight_g/weight_v) are folded at finalize.  The host data is copied; the caller may free it. */
+int dcx_set_tensor(dcx_codec* h, const char* name, const float* host_data, int32_t ndim, const int64_t* shape);
+/* Fold, pack and upload every weight; precompute codebook norms and the decode table
+ * E * W_out^T + b_out.  Blocking.  `with_generator` = 0 builds encode-side stages only. */
+int dcx_finalize(dcx_codec* h, int32_t with_generator);
+
+/* Frames for a padded clip of n_samples (= raw length + 1, distil_codec.py:133-136):
+ * T = floor((n_samples + 2*384 - 1024)/256) + 1. */
+int64_t dcx_num_frames(const dcx_codec* h, int64_t n_samples);
+/* Bytes of device workspace any stage call needs for batch B and T frames. */
+size_t dcx_workspace_size(const dcx_codec* h, int32_t batch, int64_t frames);
+
+/* log-mel front end.  Replaces LogMelSpectrogram.forward (mel_spec.py:109-122) incl. the
+ * reflect pad and the CPU-forced STFT (:26-57).  audio: [B][n_samples] (already carrying the
+ * reference's 1-sample left pad); mel: [B][T][n_mels]. */
+int dcx_mel(dcx_codec* h, const float* audio, int32_t batch, int64_t n_samples, float* mel,
+            void* workspace, size_t ws_bytes, void* stream);
+
+/* ConvNeXt encoder.  Replaces ConvNeXtEncoder.forward (encoders.py:68-76).
+ * mel: [B][T][n_mels] -> feat: [B][T][enc_dims[3]]. */
+int dcx_encode(dcx_codec* h, const float* mel, int32_t batch, int64_t frames, float* feat,
+               void* workspace, size_t ws_bytes, void* stream);
+
+/* DownsampleGRVQ.forward (grfvq.py:105-132) in eval mode: down conv + ConvNeXt block,
+ * project_in (residual_vq.py:152), nearest-code search (vector_quantize_pytorch.py:41-45,
+ * 496-506; first index on ties), gather, project_out (residual_vq.py:241), up ConvT1x1 +
+ * ConvNeXt block.  codes: [B][T] int32 (required).  x_pjt_in / quantized_fup ([B][T][3584])
+ * and quantized ([B][T][vq_dim]) may be NULL to skip them (codes-only fast path). */
+int dcx_vq_encode(dcx_codec* h, const float* feat, int32_t batch, int64_t frames, int32_t* codes,
+                  float* x_pjt_in, float* quantized_fup, float* quantized,
+                  void* workspace, size_t ws_bytes, void* stream);
+
+/* DownsampleGRVQ.decode (grfvq.py:141-146): codes [B][T] int32 -> z [B][T][vq_dim].
+ * Codes outside [0, codebook_size) are clamped to 0 and counted into *n_invalid (device int,
+ * may be NULL); the reference passes them to the gather unchecked (distil_codec.py:584-586). */
+int dcx_vq_decode(dcx_codec* h, const int32_t* codes, int32_t batch, int64_t frames, float* z,
+                  int32_t* n_invalid, void* workspace, size_t ws_bytes, void* stream);
+
+/* HiFiGANGenerator.forward (generators.py:118-147): z [B][T][gen in] -> wav [B][256*T]. */
+int dcx_generate(dcx_codec* h, const float* z, int32_t batch, int64_t frames, float* wav,
+                 void* workspace, size_t ws_bytes, void* stream);
+
+/* Whole path: audio -> mel -> encoder -> VQ -> decode(codes) -> generator (encode() followed
+ * by decode_from_codes(), distil_codec.py:545-594).  codes [B][T] and wav [B][256*T] required. */
+int dcx_encode_decode(dcx_codec* h, const float* audio, int32_t batch, int64_t n_samples,
+                      int32_t* codes, float* wav, void* workspace, size_t ws_bytes, void* stream);
+
+/* Batched 2-D transpose [B][R][C] -> [B][C][R] (channels-first <-> channels-last bridge). */
+int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int64_t cols, void* stream);
+
+/* Optional per-kernel timing: when enabled, every launch is bracketed by HIP events on its
+ * stream.  dcx_profile_read synchronises the device and returns, per kernel symbol, the
+ * launch count, summed device milliseconds and summed algorithmic FLOPs / bytes. */
+int dcx_profile_enable(dcx_codec* h, int32_t on);
+int dcx_profile_reset(dcx_codec* h);
+int32_t dcx_profile_count(const dcx_codec* h);
+int dcx_profile_read(dcx_codec* h, int32_t i, const char** name, int64_t* launches, double* ms,
+                     double* flops, double* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DISTILCODEC_AMD_H */
