@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 CSV output (kernel stats + FETCH_SIZE / WRITE_SIZE PMC passes).
+
+    python tools/rocprof_summary.py --stats DIR/run_kernel_stats.csv [--fetch DIR/run_counter_collection.csv]
+        [--write DIR/run_counter_collection.csv] [--bench-kernels kernels.json] > profiles/rNN_summary.md
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM for gfx950: FETCH_SIZE (KiB) counts half of
+a wide coalesced streaming read, so it is doubled; WRITE_SIZE (KiB) is taken as is.
+"""
+import argparse
+import csv
+import json
+import re
+from collections import defaultdict
+
+
+def short(name):
+    name = name.strip('"')
+    m = re.match(r"(?:void )?(?:dcx::)?([A-Za-z_0-9]+)(<[^()]*>)?", name)
+    if not m:
+        return name[:60]
+    base, targs = m.group(1), m.group(2) or ""
+    if base == "conv_gemm_f32":
+        parts = [p.strip() for p in targs.strip("<>").split(",")]
+        return f"{'vq_dist_argmin_f32' if parts[-1] == 'true' else 'conv_gemm_f32'}<{parts[0]},{parts[1]}>"
+    return base + targs.replace(" ", "")
+
+
+def pmc(path):
+    acc = defaultdict(lambda: [0, 0.0])
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            k = short(r["Kernel_Name"])
+            acc[k][0] += 1
+            acc[k][1] += float(r["Counter_Value"])
+    return acc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stats", required=True)
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--bench-kernels")
+    a = ap.parse_args()
+    rows = []
+    with open(a.stats) as f:
+        for r in csv.DictReader(f):
+            rows.append((short(r["Name"]), int(r["Calls"]), float(r["TotalDurationNs"]), float(r["AverageNs"]),
+                         float(r["Percentage"])))
+    fetch = pmc(a.fetch) if a.fetch else {}
+    write = pmc(a.write) if a.write else {}
+    bench = json.load(open(a.bench_kernels)) if a.bench_kernels else None
+    print("| kernel | calls | total ms | avg ms | % | HBM MB/launch (2*FETCH+WRITE) | algorithmic MB/launch |")
+    print("|---|---|---|---|---|---|---|")
+    for name, calls, tot, avg, pct in rows:
+        hbm = ""
+        if name in fetch and name in write:
+            n = fetch[name][0]
+            hbm = f"{(2 * fetch[name][1] + write[name][1]) * 1024 / n / 1e6:.1f}"
+        alg = ""
+        if bench and name in bench["kernels"]:
+            k = bench["kernels"][name]
+            alg = f"{k['bytes'] / k['launches'] / 1e6:.1f}"
+        print(f"| {name} | {calls} | {tot / 1e6:.2f} | {avg / 1e6:.4f} | {pct:.2f} | {hbm} | {alg} |")
+
+
+if __name__ == "__main__":
+    main()
