@@ -228,6 +228,7 @@ bool get_weight(dcx_codec* h, const std::string& prefix, HostTensor& out) {
 
 struct Builder {
   dcx_codec* h;
+  bool dry;  // validate names and shapes only: no device allocation
   Err e{DCX_OK, ""};
 
   bool bad() const { return e.code != DCX_OK; }
@@ -236,7 +237,7 @@ struct Builder {
   }
 
   float* upload(const std::vector<float>& v) {
-    if (bad()) return nullptr;
+    if (bad() || dry) return nullptr;
     void* p = nullptr;
     if (hipMalloc(&p, v.size() * sizeof(float) + 16) != hipSuccess) {
       set(DCX_ERR_OOM, "hipMalloc failed while uploading weights");
@@ -250,7 +251,7 @@ struct Builder {
     return (float*)p;
   }
   float* alloc(size_t n) {
-    if (bad()) return nullptr;
+    if (bad() || dry) return nullptr;
     void* p = nullptr;
     if (hipMalloc(&p, n * sizeof(float) + 16) != hipSuccess) {
       set(DCX_ERR_OOM, "hipMalloc failed");
@@ -782,11 +783,8 @@ int dcx_set_tensor(dcx_codec* h, const char* name, const float* data, int32_t nd
   return DCX_OK;
 }
 
-int dcx_finalize(dcx_codec* h, int32_t with_generator) {
-  if (!h) return DCX_ERR_INVALID_ARG;
-  if (h->finalized) return fail(h, DCX_ERR_STATE, "already finalized");
+static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
   const dcx_config& c = h->cfg;
-  Builder B{h};
   // ---- mel front end: DFT basis as a 4-tap conv over 256-sample rows ------------------
   {
     const int N = c.n_fft, nb = N / 2 + 1;
@@ -849,7 +847,7 @@ int dcx_finalize(dcx_codec* h, int32_t with_generator) {
     }
     // decode table: project_out applied to every code once, E * W_out^T + b_out
     h->ptable = B.alloc((size_t)NC * D);
-    if (!B.bad()) {
+    if (!B.bad() && !B.dry) {
       int rc = run_pointwise(h, pout, h->codebook, NC, h->ptable, 0);
       if (rc != DCX_OK) return rc;
       if (hipDeviceSynchronize() != hipSuccess) return fail(h, DCX_ERR_HIP, "decode-table build failed");
@@ -884,6 +882,18 @@ int dcx_finalize(dcx_codec* h, int32_t with_generator) {
     }
   }
   if (B.bad()) return fail(h, B.e.code, B.e.msg);
+  return DCX_OK;
+}
+
+int dcx_finalize(dcx_codec* h, int32_t with_generator) {
+  if (!h) return DCX_ERR_INVALID_ARG;
+  if (h->finalized) return fail(h, DCX_ERR_STATE, "already finalized");
+  Builder check{h, true};  // every required tensor present with the right size, before any upload
+  int rc = build_all(h, check, with_generator);
+  if (rc != DCX_OK) return rc;
+  Builder B{h, false};
+  rc = build_all(h, B, with_generator);
+  if (rc != DCX_OK) return rc;
   h->has_gen = with_generator != 0;
   h->finalized = true;
   h->host.clear();

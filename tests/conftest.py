@@ -32,4 +32,4 @@ def golden():
     import numpy as np
 
     d = os.path.join(REPO, "tests", "golden")
-    return {n: dict(np.load(os.path.join(d, f"{n}.npz"))) for n in ("e2e_batch", "e2e_3s", "modules")}
+    return {n: dict(np.load(os.path.join(d, f"{n}.npz"))) for n in ("e2e_batch", "e2e_3s", "e2e_real", "modules")}

@@ -1,0 +1,91 @@
+"""The C-ABI library loads and exports every function declared in include/distilcodec_amd.h.
+Host-only calls (no kernel launches), so this runs without a GPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "distilcodec_amd.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dcx_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_symbols_exported_and_bound():
+    from distilcodec_nabeel_amd import _native
+
+    L = _native.lib()
+    names = _declared()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(L, n), n
+        assert n in _native.SIGNATURES, f"{n} has no ctypes signature"
+    assert set(_native.SIGNATURES) == set(names)
+    assert L.dcx_abi_version() == 1
+
+
+def test_config_struct_matches_default(cfg):
+    from distilcodec_nabeel_amd import _native
+
+    L = _native.lib()
+    a = _native.DcxConfig()
+    L.dcx_default_config(ctypes.byref(a))
+    b = _native.config_from_dict(cfg)
+    assert bytes(a) == bytes(b)
+    assert list(a.up_rates)[:5] == [8, 4, 2, 2, 2] and a.codebook_size == 32768
+
+
+def test_host_queries_and_validation(cfg):
+    from distilcodec_nabeel_amd import _native
+
+    L = _native.lib()
+    c = _native.config_from_dict(cfg)
+    h = ctypes.c_void_p()
+    assert L.dcx_create(ctypes.byref(c), ctypes.byref(h)) == 0
+    try:
+        # T = floor((N + 768 - 1024) / 256) + 1 on the padded length
+        for n in (256, 24001, 72001, 240001):
+            assert L.dcx_num_frames(h, n) == (n + 768 - 1024) // 256 + 1
+        assert L.dcx_num_frames(h, 240001) == 937
+        ws = L.dcx_workspace_size(h, 32, 937)
+        gen = 6 * 32 * 937 * 8192 * 4
+        assert gen < ws < 2 * gen
+        # a stage call before finalize is a state error, not a crash
+        assert L.dcx_encode(h, None, 1, 10, None, None, 0, None) == _native.DCX_ERR_STATE
+        # finalize validates every tensor before touching the device
+        assert L.dcx_finalize(h, 1) == _native.DCX_ERR_MISSING_WEIGHT
+        assert b"encoder.downsample_layers.0.0" in L.dcx_last_error(h)
+        x = np.zeros((3,), np.float32)
+        shape = (ctypes.c_int64 * 1)(3)
+        assert L.dcx_set_tensor(h, b"encoder.norm.weight", x.ctypes.data_as(ctypes.c_void_p), 1, shape) == 0
+        assert L.dcx_set_tensor(h, None, None, 1, shape) == _native.DCX_ERR_INVALID_ARG
+    finally:
+        L.dcx_destroy(h)
+    bad = _native.config_from_dict(cfg)
+    bad.codebook_size = 1000
+    h2 = ctypes.c_void_p()
+    assert L.dcx_create(ctypes.byref(bad), ctypes.byref(h2)) == _native.DCX_ERR_INVALID_ARG
+
+
+def test_status_strings():
+    from distilcodec_nabeel_amd import _native
+
+    L = _native.lib()
+    for st in range(0, -7, -1):
+        assert L.dcx_status_string(st)
+    assert L.dcx_transpose(None, None, 1, 1, 1, None) == _native.DCX_ERR_INVALID_ARG
+
+
+def test_engine_refuses_cpu(cfg, state):
+    from distilcodec_nabeel_amd import _native
+    from distilcodec_nabeel_amd.engine import NativeCodec
+
+    with pytest.raises(_native.NativeUnavailable):
+        NativeCodec(cfg, state, "cpu")

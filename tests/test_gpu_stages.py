@@ -37,7 +37,7 @@ def _decisive(g):
     return (gap > 1e-4).reshape(g["codes"].shape)
 
 
-@pytest.mark.parametrize("name", ["e2e_batch", "e2e_3s"])
+@pytest.mark.parametrize("name", ["e2e_batch", "e2e_3s", "e2e_real"])
 def test_mel(eng, golden, name):
     g = golden[name]
     mel = eng.mel(torch.from_numpy(g["audio"]))
@@ -70,14 +70,14 @@ def test_vq_encode_on_reference_features(eng, golden, state):
 
 
 def test_vq_decode(eng, golden):
-    for name in ("e2e_batch", "e2e_3s"):
+    for name in ("e2e_batch", "e2e_3s", "e2e_real"):
         g = golden[name]
         z = eng.vq_decode(torch.from_numpy(g["codes"]))
         assert _rel(z.transpose(1, 2), g["quantized"]) < 2e-4, name
 
 
 def test_generator(eng, golden):
-    for name in ("e2e_batch", "e2e_3s"):
+    for name in ("e2e_batch", "e2e_3s", "e2e_real"):
         g = golden[name]
         wav = eng.generate(torch.from_numpy(g["quantized"]).transpose(1, 2))
         assert wav.shape == g["wav"].shape
@@ -85,7 +85,7 @@ def test_generator(eng, golden):
         assert snr >= 80, (name, snr)
 
 
-@pytest.mark.parametrize("name", ["e2e_batch", "e2e_3s"])
+@pytest.mark.parametrize("name", ["e2e_batch", "e2e_3s", "e2e_real"])
 def test_encode_decode_end_to_end(eng, golden, name):
     g = golden[name]
     codes, wav = eng.encode_decode(torch.from_numpy(g["audio"]))

@@ -61,7 +61,7 @@ def test_modules(golden, state, cfg):
         assert np.array_equal(emb[idx].numpy(), m["vq1024_quant"])
 
 
-@pytest.mark.parametrize("name", ["e2e_batch", "e2e_3s"])
+@pytest.mark.parametrize("name", ["e2e_batch", "e2e_3s", "e2e_real"])
 def test_end_to_end(golden, state, cfg, name):
     g = golden[name]
     torch.set_num_threads(8)
