@@ -36,8 +36,23 @@ from distilcodec_nabeel_amd import synth, weights  # noqa: E402
 from distilcodec_nabeel_amd.engine import NativeCodec  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (= fp32 vector peak)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
+# x6 mode executes 6 exact bf16 products per fp32 product: its ceiling in fp32-algorithmic FLOP/s
+X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
 HBM_PEAK_GBS = 8000.0
 SR = 24000
+
+
+def traffic_for(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass (profiles/pmc_latest.json:
+    2*FETCH_SIZE + WRITE_SIZE, gfx950 correction), or None when that kernel was not profiled."""
+    path = os.path.join(HERE, "profiles", "pmc_latest.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def cpu_baseline(cfg, state, seconds: float, batch: int):
@@ -68,6 +83,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-batch", type=int, default=2)
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch HIP-event roofline timing")
+    ap.add_argument("--gemm", choices=["x6", "f32"], default="x6",
+                    help="x6: fp32 operands as 3 bf16 planes, 6 exact products, f32 accumulate; f32: fp32 MFMA")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -80,7 +97,7 @@ def main():
 
     cfg = dconfig.default_config()
     state = weights.synthetic_state_dict(cfg, seed=1234)
-    eng = NativeCodec(cfg, state, dev)
+    eng = NativeCodec(cfg, state, dev, gemm=args.gemm)
 
     n = int(args.seconds * SR)
     clips = synth.clips(args.batch, n, seed=1000 * rank, kind="mix")
@@ -129,8 +146,11 @@ def main():
         name, rec = max(prof.items(), key=lambda kv: kv[1]["ms"])
         avg_ms = rec["ms"] / rec["launches"]
         achieved = rec["flops"] / (rec["ms"] * 1e-3) / 1e12
-        roof = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+        peak = X6_PEAK_TFLOPS if "x6" in name else FP32_MFMA_PEAK_TFLOPS
+        roof = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": round(peak, 1),
+                "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic_for(name),
+                "peak_basis": ("bf16 dense MFMA 2500 TF / 6 bf16 products per fp32 product" if "x6" in name
+                               else "fp32 MFMA v_mfma_f32_32x32x2_f32"),
                 "launches_per_step": rec["launches"] // args.steps, "avg_launch_ms": round(avg_ms, 4),
                 "share_of_device_time": round(rec["ms"] / sum(r["ms"] for r in prof.values()), 4)}
         if rank == 0 and os.environ.get("DCX_BENCH_KERNELS"):
@@ -154,6 +174,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "arith": ("fp32 operands split into 3 bf16 planes, 6 exact bf16 products per fp32 product, fp32 "
+                      "accumulation (v_mfma_f32_32x32x16_bf16)" if args.gemm == "x6" else
+                      "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
             "data": "synthetic (speech/music-like 24 kHz clips; seeded synthetic weights, no checkpoint offline)",
             "config": {"workload": f"C2: {args.batch} x {args.seconds:g} s clips per GPU, full mel->encoder->VQ->"
                                    f"decode->generator, fp32", "global_batch": args.batch * world,

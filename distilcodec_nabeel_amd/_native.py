@@ -12,7 +12,7 @@ import os
 
 import torch  # noqa: F401  (see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdcx.so")
+LIB_PATH = os.environ.get("DCX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdcx.so")
 
 DCX_OK = 0
 DCX_ERR_INVALID_ARG = -1
@@ -21,6 +21,8 @@ DCX_ERR_STATE = -3
 DCX_ERR_HIP = -4
 DCX_ERR_OOM = -5
 DCX_ERR_WORKSPACE = -6
+DCX_GEMM_F32 = 0
+DCX_GEMM_X6 = 1
 
 
 class NativeUnavailable(RuntimeError):
@@ -72,6 +74,11 @@ SIGNATURES = {
     "dcx_generate": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _SZ, _P]),
     "dcx_encode_decode": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _SZ, _P]),
     "dcx_transpose": (ctypes.c_int, [_P, _P, _I32, _I64, _I64, _P]),
+    "dcx_set_gemm_mode": (ctypes.c_int, [_P, _I32]),
+    "dcx_get_gemm_mode": (_I32, [_P]),
+    "dcx_conv_create": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, ctypes.POINTER(_P)]),
+    "dcx_conv_forward": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, _P, _P, _P, _I32, _P]),
+    "dcx_conv_destroy": (None, [_P]),
     "dcx_profile_enable": (ctypes.c_int, [_P, _I32]),
     "dcx_profile_reset": (ctypes.c_int, [_P]),
     "dcx_profile_count": (_I32, [_P]),

@@ -35,6 +35,7 @@ struct HostTensor {
 
 struct ConvW {
   float* w = nullptr;
+  unsigned short* w6 = nullptr;  // bf16 3-plane split, x6 kernel layout
   float* b = nullptr;
   int cin = 0, cout = 0, taps = 1, phases = 1, in_step = 1, out_mul = 1;
   int in_base[dcx::kMaxPhases] = {0};
@@ -99,6 +100,8 @@ struct dcx_codec {
   ConvW vq_down, vq_pin, vq_up;
   BlockW vq_down_blk, vq_up_blk;
   float *codebook = nullptr, *e2 = nullptr, *ptable = nullptr;
+  unsigned short* codebook6 = nullptr;
+  int gemm_mode = DCX_GEMM_X6;
 
   ConvW conv_pre;
   ConvW ups[8];
@@ -226,6 +229,26 @@ bool get_weight(dcx_codec* h, const std::string& prefix, HostTensor& out) {
   return false;
 }
 
+unsigned short bf16_rne(float x) {
+  unsigned u;
+  std::memcpy(&u, &x, 4);
+  return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+float bf16_f(unsigned short b) {
+  unsigned u = (unsigned)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+// x = hi + mid + lo, the same split the x6 kernel applies to activations.
+void split3_host(float x, unsigned short& h, unsigned short& m, unsigned short& l) {
+  h = bf16_rne(x);
+  const float r1 = x - bf16_f(h);
+  m = bf16_rne(r1);
+  const float r2 = r1 - bf16_f(m);
+  l = bf16_rne(r2);
+}
+
 struct Builder {
   dcx_codec* h;
   bool dry;  // validate names and shapes only: no device allocation
@@ -249,6 +272,42 @@ struct Builder {
       return nullptr;
     }
     return (float*)p;
+  }
+  unsigned short* upload16(const std::vector<unsigned short>& v) {
+    if (bad() || dry) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, v.size() * sizeof(unsigned short) + 16) != hipSuccess) {
+      set(DCX_ERR_OOM, "hipMalloc failed while uploading split weights");
+      return nullptr;
+    }
+    h->allocs.push_back(p);
+    if (hipMemcpy(p, v.data(), v.size() * sizeof(unsigned short), hipMemcpyHostToDevice) != hipSuccess) {
+      set(DCX_ERR_HIP, "hipMemcpy failed while uploading split weights");
+      return nullptr;
+    }
+    return (unsigned short*)p;
+  }
+  // fp32 packed [phases][cout][taps][cin] -> x6 layout [phase][tap][cin/16][cout][2][3][8] bf16
+  unsigned short* split_pack(const std::vector<float>& pk, int phases, int cout, int taps, int cin) {
+    if (bad() || dry) return nullptr;
+    const int nch = cin / 16;
+    std::vector<unsigned short> out((size_t)phases * taps * nch * cout * 48);
+    for (int r = 0; r < phases; ++r)
+      for (int m = 0; m < taps; ++m)
+        for (int c = 0; c < nch; ++c)
+          for (int o = 0; o < cout; ++o) {
+            unsigned short* dst = &out[((((size_t)r * taps + m) * nch + c) * cout + o) * 48];
+            const float* src = &pk[(((size_t)r * cout + o) * taps + m) * cin + c * 16];
+            for (int hh = 0; hh < 2; ++hh)
+              for (int j = 0; j < 8; ++j) {
+                unsigned short a, b2, c2;
+                split3_host(src[hh * 8 + j], a, b2, c2);
+                dst[hh * 24 + 0 + j] = a;
+                dst[hh * 24 + 8 + j] = b2;
+                dst[hh * 24 + 16 + j] = c2;
+              }
+          }
+    return upload16(out);
   }
   float* alloc(size_t n) {
     if (bad() || dry) return nullptr;
@@ -301,6 +360,7 @@ struct Builder {
       for (int i = 0; i < cin; ++i)
         for (int j = 0; j < k; ++j) pk[((size_t)o * k + j) * cin + i] = w.data[((size_t)o * cin + i) * k + j];
     c.w = upload(pk);
+    if (cin % 16 == 0) c.w6 = split_pack(pk, 1, cout, k, cin);
     if (has_bias) c.b = vec(prefix + ".bias", cout);
     return c;
   }
@@ -323,6 +383,7 @@ struct Builder {
             pk[(((size_t)r * cout + o) * taps + m) * cin + i] = w.data[((size_t)i * cout + o) * k + jr + m * s];
     }
     c.w = upload(pk);
+    if (cin % 16 == 0) c.w6 = split_pack(pk, s, cout, taps, cin);
     c.b = vec(prefix + ".bias", cout);
     return c;
   }
@@ -419,6 +480,7 @@ int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s) {
   ConvParams p{};
   p.x = c.x;
   p.w = w.w;
+  p.w6 = h->gemm_mode == DCX_GEMM_X6 ? w.w6 : nullptr;
   p.bias = w.b;
   p.gamma = c.gamma;
   p.res = c.res;
@@ -558,7 +620,7 @@ int stage_vq_encode(dcx_codec* h, const float* feat, int B, int T, int32_t* code
   LAUNCH(h, s, "row_sqnorm", 2.0 * M * CD, 4.0 * M * CD, dcx::launch_row_sqnorm(P, M, CD, x2, s));
   {
     ConvParams p{};
-    p.x = P; p.w = h->codebook; p.Cin = CD; p.Cout = NC; p.ldx = CD; p.taps = 1; p.in_step = 1; p.out_mul = 1;
+    p.x = P; p.w = h->codebook; p.w6 = h->gemm_mode == DCX_GEMM_X6 ? h->codebook6 : nullptr; p.Cin = CD; p.Cout = NC; p.ldx = CD; p.taps = 1; p.in_step = 1; p.out_mul = 1;
     p.x2 = x2; p.e2 = h->e2; p.part_val = pv; p.part_idx = pi;
     ProfScope ps(h, s);
     const char* kname = "vq";
@@ -799,6 +861,7 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
       }
     h->dft.cin = c.hop; h->dft.cout = N; h->dft.taps = N / c.hop; h->dft.in_step = 1;
     h->dft.w = B.upload(basis);
+    h->dft.w6 = B.split_pack(basis, 1, N, N / c.hop, c.hop);
     const int kpad = (nb + 15) / 16 * 16;
     std::vector<double> fb = mel_fb(nb, c.f_min, c.f_max, c.n_mels, c.sample_rate);
     std::vector<float> pk((size_t)c.n_mels * kpad, 0.f);
@@ -806,6 +869,7 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
       for (int k = 0; k < nb; ++k) pk[(size_t)m * kpad + k] = (float)fb[(size_t)k * c.n_mels + m];
     h->melfb.cin = kpad; h->melfb.cout = c.n_mels; h->melfb.taps = 1;
     h->melfb.w = B.upload(pk);
+    h->melfb.w6 = B.split_pack(pk, 1, c.n_mels, 1, kpad);
   }
   // ---- encoder --------------------------------------------------------------------------
   {
@@ -843,6 +907,7 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
         e2[i] = (float)sacc;
       }
       h->codebook = B.upload(emb->data);
+      h->codebook6 = B.split_pack(emb->data, 1, NC, 1, CD);
       h->e2 = B.upload(e2);
     }
     // decode table: project_out applied to every code once, E * W_out^T + b_out
@@ -971,6 +1036,75 @@ int dcx_encode_decode(dcx_codec* h, const float* audio, int32_t batch, int64_t n
 int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int64_t cols, void* stream) {
   if (!in || !out || batch <= 0 || rows <= 0 || cols <= 0) return DCX_ERR_INVALID_ARG;
   return dcx::launch_transpose(in, out, batch, rows, cols, (hipStream_t)stream) == hipSuccess ? DCX_OK : DCX_ERR_HIP;
+}
+
+int dcx_set_gemm_mode(dcx_codec* h, int32_t mode) {
+  if (!h) return DCX_ERR_INVALID_ARG;
+  if (mode != DCX_GEMM_F32 && mode != DCX_GEMM_X6) return fail(h, DCX_ERR_INVALID_ARG, "unknown GEMM mode");
+  h->gemm_mode = mode;
+  return DCX_OK;
+}
+
+int32_t dcx_get_gemm_mode(const dcx_codec* h) { return h ? h->gemm_mode : -1; }
+
+}  // extern "C"
+
+struct dcx_conv {
+  dcx_codec scratch;  // owns the device allocations and the last error
+  ConvW w;
+};
+
+extern "C" {
+
+int dcx_conv_create(const float* weight, const float* bias, int32_t cin, int32_t cout, int32_t k, int32_t dilation,
+                    int32_t transposed, int32_t stride, dcx_conv** out) {
+  if (!weight || !out || cin <= 0 || cout <= 0 || k <= 0 || dilation <= 0 || stride <= 0) return DCX_ERR_INVALID_ARG;
+  if (cin % 16 || cout % 32) return DCX_ERR_INVALID_ARG;
+  if (transposed && (k % stride || (k - stride) % 2 || stride > dcx::kMaxPhases)) return DCX_ERR_INVALID_ARG;
+  if (!transposed && (k % 2 == 0)) return DCX_ERR_INVALID_ARG;
+  auto c = new (std::nothrow) dcx_conv();
+  if (!c) return DCX_ERR_OOM;
+  dcx_codec* h = &c->scratch;
+  HostTensor wt;
+  const int64_t n = (int64_t)cin * cout * k;
+  wt.shape = transposed ? std::vector<int64_t>{cin, cout, k} : std::vector<int64_t>{cout, cin, k};
+  wt.data.assign(weight, weight + n);
+  h->host["c.weight"] = wt;
+  HostTensor bt;
+  bt.shape = {cout};
+  if (bias) bt.data.assign(bias, bias + cout); else bt.data.assign(cout, 0.f);
+  h->host["c.bias"] = bt;
+  Builder B{h, false};
+  c->w = transposed ? B.convT("c", cin, cout, k, stride) : B.conv("c", cin, cout, k, dilation, dilation * (k - 1) / 2);
+  h->host.clear();
+  if (B.bad()) {
+    int code = B.e.code;
+    dcx_conv_destroy(c);
+    return code;
+  }
+  *out = c;
+  return DCX_OK;
+}
+
+int dcx_conv_forward(dcx_conv* c, int32_t gemm_mode, const float* x, int32_t batch, int64_t lin, float* y,
+                     float* y_silu, const float* res, int32_t epi, void* stream) {
+  if (!c || !x || batch <= 0 || lin <= 0 || (!y && !y_silu)) return DCX_ERR_INVALID_ARG;
+  if (epi != dcx::EPI_BIAS && epi != dcx::EPI_GELU && epi != dcx::EPI_RES) return DCX_ERR_INVALID_ARG;
+  if (epi == dcx::EPI_RES && !res) return DCX_ERR_INVALID_ARG;
+  dcx_codec* h = &c->scratch;
+  h->gemm_mode = gemm_mode;
+  ConvCall cc{x, (long long)lin * c->w.cin, batch, (int)lin, (int)lin, c->w.cin};
+  cc.y = y;
+  cc.y2 = y_silu;
+  cc.res = res;
+  cc.epi = epi;
+  return run_conv(h, c->w, cc, (hipStream_t)stream);
+}
+
+void dcx_conv_destroy(dcx_conv* c) {
+  if (!c) return;
+  for (void* p : c->scratch.allocs) hipFree(p);
+  delete c;
 }
 
 int dcx_profile_enable(dcx_codec* h, int32_t on) {

@@ -1,4 +1,4 @@
-// Implicit-GEMM 1-D convolution on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+// Implicit-GEMM 1-D convolution on gfx950 matrix cores.
 //
 // One kernel family serves every contraction on the DistilCodec path:
 //   Conv1d k>1 / dilated (stem k7, conv_pre k13, ResBlock1 k3/7/11 x dil 1/3/5),
@@ -8,25 +8,36 @@
 //
 // GEMM view: rows = output time positions q (M), cols = output channels (N),
 // K = taps x Cin.  Channels-last activations make every A-tile row a contiguous Cin slice and
-// every store a contiguous Cout slice (coalesced); the weight tile is [Cout][taps*Cin].
+// every store a contiguous Cout slice (coalesced).
 //
-// MFMA fragment maps (cdna_hip_programming.md §3): for 32x32x2 f32, lane l supplies
-// A[i=l&31][k=l>>5] and B[k=l>>5][j=l&31]; C/D: col=l&31, row=(r&3)+8*(r>>2)+4*(l>>5).
-// Within each 16-deep K chunk, lane half h owns k = 8h..8h+7 (k-step s uses k = 8h+s), so a
-// fragment is two ds_read_b128 of 8 consecutive k.  LDS rows are padded to 20 floats, which
-// makes those reads conflict-free (20*i mod 64 distinct over every 16-lane b128 group).
+// Two arithmetic modes, identical epilogues:
+//  * conv_gemm_f32: v_mfma_f32_32x32x2_f32 (exact fp32 fmaf chain, 157 TF peak).
+//  * conv_gemm_x6:  fp32-accurate 3-plane bf16 split.  Every fp32 operand x is held as
+//    x = hi + mid + lo (three bf16, RNE; residual <= 2^-27|x|) and a product uses the six terms
+//    hi*hi + hi*mid + mid*hi + hi*lo + mid*mid + lo*hi, each exact in fp32 (8x8-bit
+//    significands), accumulated in fp32 by v_mfma_f32_32x32x16_bf16.  The dropped terms are
+//    <= 2^-24 relative, i.e. fp32 rounding level; the MFMA ceiling is 16/6 = 2.67x the fp32 one.
+//    Weights are split once at load; activations are split while being staged into LDS, and
+//    each staged input tile (with its tap halo) serves every tap of the conv.
 //
-// Pipeline: register-staged double buffer, one barrier per K chunk: the global loads for chunk
-// k+1 are issued before the MFMAs of chunk k and written to the other LDS buffer after them.
+// MFMA fragment maps (cdna_hip_programming.md §3): 32x32x2 f32: lane l supplies A[l&31][k=l>>5]
+// and B[k=l>>5][l&31]; 32x32x16 bf16: A[l&31][k=8(l>>5)+j], B[k=8(l>>5)+j][l&31], j<8;
+// C/D for both: col=l&31, row=(r&3)+8*(r>>2)+4*(l>>5).
+#include <type_traits>
+
 #include "dcx_kernels.h"
 
 namespace dcx {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int BK = 16;    // K chunk per pipeline stage
-constexpr int LDSK = 20;  // padded LDS row (floats)
+constexpr int BK = 16;    // K chunk per pipeline stage (both modes)
+constexpr int LDSK = 20;  // f32 mode: padded LDS row (floats); 20*i mod 64 distinct per b128 group
+constexpr int XROW = 56;  // x6 mode: LDS row = [half 2][plane 3][8] bf16 + 8 pad (112 B; 28*i mod 64 distinct)
 
 __device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
 __device__ __forceinline__ float gelu_f(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f)); }
@@ -39,6 +50,130 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+// Zero page read in place of out-of-range input rows (conv zero padding): selecting the address
+// instead of the loaded value keeps every staging load unconditional, so hipcc neither branches
+// around it nor waits vmcnt(0) after it (cdna_hip_programming.md §5, trap 4(c)).
+__device__ __attribute__((aligned(16))) float g_zero_row[BK] = {0.f};
+
+// RNE fp32 -> bf16 bits (finite inputs) and back.
+__device__ __forceinline__ unsigned short bf16_bits(float x) {
+  const unsigned u = __float_as_uint(x);
+  return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf16_val(unsigned short b) { return __uint_as_float((unsigned)b << 16); }
+
+// x -> (hi, mid, lo) bf16 planes.
+__device__ __forceinline__ void split3(float x, unsigned short& h, unsigned short& m, unsigned short& l) {
+#ifdef DCX_EXP_NOSPLIT  // timing experiment only: wrong results
+  h = (unsigned short)(__float_as_uint(x) >> 16); m = h; l = h; return;
+#endif
+  h = bf16_bits(x);
+  const float r1 = x - bf16_val(h);
+  m = bf16_bits(r1);
+  const float r2 = r1 - bf16_val(m);
+  l = bf16_bits(r2);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Shared epilogue: per-element ops of the conv / argmin of the VQ search.
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, bool ARGMIN>
+__device__ __forceinline__ void epilogue(const ConvParams& p, f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int q0,
+                                         int co0, int nt, int ntiles, int b, int ph, float* smem) {
+  constexpr int WR = BM / WM, WC = BN / WN;
+  constexpr int TM = WR / 32, TN = WC / 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lrow = lane & 31;
+  const int rhalf = 4 * (lane >> 5);
+  if constexpr (!ARGMIN) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int co = co0 + wn * WC + j * 32 + lrow;
+        const float bias = p.bias ? p.bias[co] : 0.f;
+        const float gam = (p.epi == EPI_GAMMA_RES) ? p.gamma[co] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = q0 + wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + rhalf;
+          if (q >= p.Lq) continue;
+          const long long o = (long long)b * p.y_bstride + (long long)(q * p.out_mul + ph) * p.ldy + co;
+          float v = acc[i][j][r] + bias;
+          switch (p.epi) {
+            case EPI_GELU: v = gelu_f(v); break;
+            case EPI_GAMMA_RES: v = p.res[o] + gam * v; break;
+            case EPI_RES: v = p.res[o] + v; break;
+            case EPI_LOGCLAMP: v = logf(fmaxf(v, 1e-5f)); break;
+            default: break;
+          }
+          if (p.mean_mode == MEAN_FIRST) {
+            p.macc[o] = v;
+            continue;
+          } else if (p.mean_mode == MEAN_MID) {
+            p.macc[o] = p.macc[o] + v;
+            continue;
+          } else if (p.mean_mode == MEAN_LAST) {
+            v = (p.macc[o] + v) / 3.0f;
+          }
+          if (p.y) p.y[o] = v;
+          if (p.y2) p.y2[o] = silu_f(v);
+        }
+      }
+  } else {
+    // VQ search: dist = sqrt(clamp((|x|^2 + |e|^2) + (-2 x.e), 0)) exactly in the reference's
+    // operation order (vector_quantize_pytorch.py:41-45); per row keep the smallest distance,
+    // lowest code index on ties (torch argmax of -dist returns the first).
+    __syncthreads();
+    float* rv = smem;                                  // [WN][BM]
+    int* ri = reinterpret_cast<int*>(smem + WN * BM);  // [WN][BM]
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rloc = wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + rhalf;
+        const int q = q0 + rloc;
+        const float xx = (q < p.Lq) ? p.x2[(long long)b * p.Lq + q] : 0.f;
+        float bv = __builtin_inff();
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int co = co0 + wn * WC + j * 32 + lrow;
+          const float d2 = (xx + p.e2[co]) + (-2.0f * acc[i][j][r]);
+          const float d = sqrtf(fmaxf(d2, 0.0f));
+          if (d < bv || (d == bv && co < bi)) { bv = d; bi = co; }
+        }
+#pragma unroll
+        for (int off = 16; off >= 1; off >>= 1) {
+          const float ov = __shfl_xor(bv, off, 64);
+          const int oi = __shfl_xor(bi, off, 64);
+          if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+        }
+        if (lrow == 0) { rv[wn * BM + rloc] = bv; ri[wn * BM + rloc] = bi; }
+      }
+    }
+    __syncthreads();
+    for (int rloc = tid; rloc < BM; rloc += 256) {
+      const int q = q0 + rloc;
+      if (q >= p.Lq) continue;
+      float bv = rv[rloc];
+      int bi = ri[rloc];
+#pragma unroll
+      for (int w = 1; w < WN; ++w) {
+        const float ov = rv[w * BM + rloc];
+        const int oi = ri[w * BM + rloc];
+        if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      const long long o = ((long long)b * p.Lq + q) * ntiles + nt;
+      p.part_val[o] = bv;
+      p.part_idx[o] = bi;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// fp32 MFMA kernel.  Register-staged double buffer, one barrier per 16-deep K chunk.
+// ---------------------------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, bool ARGMIN>
 __global__ void __launch_bounds__(256) conv_gemm_f32(const ConvParams p) {
   static_assert(WM * WN == 4, "4 waves per workgroup");
@@ -150,125 +285,270 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const ConvParams p) {
     if (kt + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
   }
+  epilogue<BM, BN, WM, WN, ARGMIN>(p, acc, q0, co0, nt, ntiles, b, ph, smem);
+}
 
-  const int rhalf = 4 * (lane >> 5);
-  if constexpr (!ARGMIN) {
+// ---------------------------------------------------------------------------------------------
+// x6, 8-wave variant (512 threads, 2 waves per SIMD), block tile 256 x 128, wave tile 64 x 64.
+// Same arithmetic and LDS images as conv_gemm_x6; the loads run two K16 steps ahead of their use
+// (two register sets, loop unrolled by two), so a step's MFMAs (2 waves x 24 per SIMD = 1536
+// cycles) cover the L2 / Infinity-Cache latency of the tiles two steps out.
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN>
+__global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
+  static_assert(WM * WN == 8, "8 waves per workgroup");
+  constexpr int WR = BM / WM, WC = BN / WN;
+  constexpr int TM = WR / 32, TN = WC / 32;
+  constexpr int AROWS = BM + HALO;
+  constexpr int A_F4 = AROWS * 4;
+  constexpr int B_P = BN * 6;
+  constexpr int A_PT = (A_F4 + 511) / 512, B_PT = (B_P + 511) / 512;
+  constexpr int ABUF = AROWS * XROW, BBUF = BN * XROW;
+
+  // LDS: input tiles (2, by chunk parity) + weight-tile ring (3, by step mod 3).
+  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * ABUF + 3 * BBUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int ntiles = p.Cout / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = wg / ntiles, nt = wg - mt * ntiles;
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int b = blockIdx.y, ph = blockIdx.z;
+  const float* __restrict__ xb = p.x + (long long)b * p.x_bstride;
+  const int nchunks = p.Cin / BK;
+  const int taps = p.taps;
+  const int nsteps = nchunks * taps;
+  const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
+  const int row0 = q0 + p.in_base[ph] + lo_rel;
+  const unsigned short* __restrict__ wbase =
+      p.w6 + ((long long)ph * taps * nchunks) * p.Cout * 48 + (long long)co0 * 48;
+  const long long wslab = (long long)p.Cout * 48;
+  const int lin = p.Lin;
+
+  // Branch-free staging slots (surplus slots duplicate the last element).
+  int a_row[A_PT], a_col[A_PT];
+#pragma unroll
+  for (int i = 0; i < A_PT; ++i) {
+    const int idx = min(tid + 512 * i, A_F4 - 1);
+    a_row[i] = idx >> 2;
+    a_col[i] = idx & 3;
+  }
+  int b_off[B_PT], b_lds[B_PT];
+#pragma unroll
+  for (int i = 0; i < B_PT; ++i) {
+    const int idx = min(tid + 512 * i, B_P - 1);
+    const int col = idx / 6, piece = idx - col * 6;
+    b_off[i] = idx * 8;
+    b_lds[i] = col * XROW + piece * 8;
+  }
+
+  f32x4 ra[2][A_PT];
+  f32x4 rb[2][B_PT];
+
+  auto loadA = [&](int c, f32x4(&r)[A_PT]) {
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) {
+      const int ir = row0 + a_row[i];
+      const bool ok = ir >= 0 && ir < lin;
+      const float* src = ok ? xb + (long long)ir * p.ldx + c * BK + a_col[i] * 4 : g_zero_row + a_col[i] * 4;
+      r[i] = *reinterpret_cast<const f32x4*>(src);
+    }
+  };
+  auto storeA = [&](int buf, const f32x4(&r)[A_PT]) {
+    unsigned short* A = lds + buf * ABUF;
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) {
+      s16x4 hv, mv, lv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        unsigned short h, m, l;
+        split3(r[i][e], h, m, l);
+        hv[e] = (short)h; mv[e] = (short)m; lv[e] = (short)l;
+      }
+      unsigned short* dst = A + a_row[i] * XROW + (a_col[i] >> 1) * 24 + (a_col[i] & 1) * 4;
+      *reinterpret_cast<s16x4*>(dst) = hv;
+      *reinterpret_cast<s16x4*>(dst + 8) = mv;
+      *reinterpret_cast<s16x4*>(dst + 16) = lv;
+    }
+  };
+  auto loadB = [&](int c, int m, f32x4(&r)[B_PT]) {
+    const unsigned short* src = wbase + ((long long)m * nchunks + c) * wslab;
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) r[i] = *reinterpret_cast<const f32x4*>(src + b_off[i]);
+  };
+  auto storeB = [&](int slot, const f32x4(&r)[B_PT]) {
+    unsigned short* Bsm = lds + 2 * ABUF + slot * BBUF;
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) *reinterpret_cast<f32x4*>(Bsm + b_lds[i]) = r[i];
+  };
+
+  const int lrow = lane & 31;
+  const int hoff = (lane >> 5) * 24;
+  s16x8 af[2][TM][3], bfr[2][TN][3];
+  // fragments of step (c, m) in ring slot `slot` -> register set F
+  auto readF = [&](int c, int m, int slot, s16x8(&a)[TM][3], s16x8(&bb)[TN][3]) {
+    const int off = m * p.in_step - lo_rel;
+    const unsigned short* A = lds + (c & 1) * ABUF;
+    const unsigned short* Bsm = lds + 2 * ABUF + slot * BBUF;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const unsigned short* ap = A + (wm * WR + i * 32 + lrow + off) * XROW + hoff;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const s16x8*>(ap + pl * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const unsigned short* bp = Bsm + (wn * WC + j * 32 + lrow) * XROW + hoff;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) bb[j][pl] = *reinterpret_cast<const s16x8*>(bp + pl * 8);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto adv = [&](int& c_, int& m_) {
+    if (++m_ == taps) { m_ = 0; ++c_; }
+  };
+  // ---- prologue: A(0), B(0), B(1) (and A(1) when taps == 1) in LDS; the next loads in flight
+  loadA(0, ra[0]);
+  loadB(0, 0, rb[0]);
+  storeA(0, ra[0]);
+  storeB(0, rb[0]);
+  int c1 = 0, m1 = 0;  // position of step s+1
+  adv(c1, m1);
+  if (nsteps > 1) {
+    loadB(c1, m1, rb[0]);
+    storeB(1, rb[0]);
+  }
+  if (taps == 1 && nchunks > 1) {
+    loadA(1, ra[0]);
+    storeA(1, ra[0]);
+  }
+  int c2 = c1, m2 = m1;  // position of step s+2
+  adv(c2, m2);
+  int c3 = c2, m3 = m2;  // position of step s+3
+  adv(c3, m3);
+  // in flight for the first loop step: B(2) and the input chunk first used at step 2
+  loadB(min(c2, nchunks - 1), c2 < nchunks ? m2 : taps - 1, rb[1]);
+  if (m2 == 0 && c2 < nchunks) loadA(c2, ra[1]);
+  __syncthreads();
+  readF(0, 0, 0, af[0], bfr[0]);
+
+  int c = 0, slot = 0;  // chunk of step s; ring slot of step s
+  auto step = [&](int s, auto qtag) {
+    constexpr int Q = decltype(qtag)::value;
+    const int slot1 = slot == 2 ? 0 : slot + 1, slot2 = slot1 == 2 ? 0 : slot1 + 1;
+    // 1. fragments of step s+1 (its data was made visible by the previous barrier)
+    if (s + 1 < nsteps) readF(c1, m1, slot1, af[1 - Q], bfr[1 - Q]);
+    // 2. global loads for step s+3 (B) and for the input chunk first used at step s+3
+    loadB(min(c3, nchunks - 1), c3 < nchunks ? m3 : taps - 1, rb[Q]);
+    if (m3 == 0 && c3 < nchunks) loadA(c3, ra[Q]);
+    // 3. MFMAs of step s
+#define DCX_MF(i, j, x, y) \
+  acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[Q][i][x]), \
+                                                      __builtin_bit_cast(bf16x8, bfr[Q][j][y]), acc[i][j], 0, 0, 0)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int co = co0 + wn * WC + j * 32 + lrow;
-        const float bias = p.bias ? p.bias[co] : 0.f;
-        const float gam = (p.epi == EPI_GAMMA_RES) ? p.gamma[co] : 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int q = q0 + wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + rhalf;
-          if (q >= p.Lq) continue;
-          const long long o = (long long)b * p.y_bstride + (long long)(q * p.out_mul + ph) * p.ldy + co;
-          float v = acc[i][j][r] + bias;
-          switch (p.epi) {
-            case EPI_GELU: v = gelu_f(v); break;
-            case EPI_GAMMA_RES: v = p.res[o] + gam * v; break;
-            case EPI_RES: v = p.res[o] + v; break;
-            case EPI_LOGCLAMP: v = logf(fmaxf(v, 1e-5f)); break;
-            default: break;
-          }
-          if (p.mean_mode == MEAN_FIRST) {
-            p.macc[o] = v;
-            continue;
-          } else if (p.mean_mode == MEAN_MID) {
-            p.macc[o] = p.macc[o] + v;
-            continue;
-          } else if (p.mean_mode == MEAN_LAST) {
-            v = (p.macc[o] + v) / 3.0f;
-          }
-          if (p.y) p.y[o] = v;
-          if (p.y2) p.y2[o] = silu_f(v);
-        }
+        DCX_MF(i, j, 2, 0);
+        DCX_MF(i, j, 1, 1);
+        DCX_MF(i, j, 0, 2);
+        DCX_MF(i, j, 1, 0);
+        DCX_MF(i, j, 0, 1);
+        DCX_MF(i, j, 0, 0);
       }
-  } else {
-    // VQ search epilogue: dist = sqrt(clamp((|x|^2 + |e|^2) + (-2 x.e), 0)) exactly in the
-    // reference's operation order (vector_quantize_pytorch.py:41-45); per row keep the
-    // smallest distance, lowest code index on ties (torch argmax of -dist returns the first).
+#undef DCX_MF
+    // 4. stage step s+2: weight tile into its ring slot; its input chunk if s+2 opens one
+    storeB(slot2, rb[1 - Q]);
+    if (m2 == 0 && c2 < nchunks) storeA(c2 & 1, ra[1 - Q]);
     __syncthreads();
-    float* rv = smem;                                        // [WN][BM]
-    int* ri = reinterpret_cast<int*>(smem + WN * BM);        // [WN][BM]
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rloc = wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + rhalf;
-        const int q = q0 + rloc;
-        const float xx = (q < p.Lq) ? p.x2[(long long)b * p.Lq + q] : 0.f;
-        float bv = __builtin_inff();
-        int bi = 0x7fffffff;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int co = co0 + wn * WC + j * 32 + lrow;
-          const float d2 = (xx + p.e2[co]) + (-2.0f * acc[i][j][r]);
-          const float d = sqrtf(fmaxf(d2, 0.0f));
-          if (d < bv || (d == bv && co < bi)) { bv = d; bi = co; }
-        }
-#pragma unroll
-        for (int off = 16; off >= 1; off >>= 1) {
-          const float ov = __shfl_xor(bv, off, 64);
-          const int oi = __shfl_xor(bi, off, 64);
-          if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-        }
-        if (lrow == 0) { rv[wn * BM + rloc] = bv; ri[wn * BM + rloc] = bi; }
-      }
-    }
-    __syncthreads();
-    for (int rloc = tid; rloc < BM; rloc += 256) {
-      const int q = q0 + rloc;
-      if (q >= p.Lq) continue;
-      float bv = rv[rloc];
-      int bi = ri[rloc];
-#pragma unroll
-      for (int w = 1; w < WN; ++w) {
-        const float ov = rv[w * BM + rloc];
-        const int oi = ri[w * BM + rloc];
-        if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-      }
-      const long long o = ((long long)b * p.Lq + q) * ntiles + nt;
-      p.part_val[o] = bv;
-      p.part_idx[o] = bi;
-    }
+    adv(c1, m1);
+    adv(c2, m2);
+    adv(c3, m3);
+    slot = slot1;
+    (void)c;
+  };
+  for (int s = 0; s < nsteps; s += 2) {
+    step(s, std::integral_constant<int, 0>{});
+    if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>{});
   }
+  epilogue<BM, BN, WM, WN, ARGMIN>(p, acc, q0, co0, nt, ntiles, b, ph, reinterpret_cast<float*>(lds));
 }
 
+// ---------------------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, bool ARGMIN>
-static hipError_t launch_tile(const ConvParams& p, int batch, int phases, hipStream_t s) {
+static hipError_t launch_f32(const ConvParams& p, int batch, int phases, hipStream_t s) {
   const int mtiles = (p.Lq + BM - 1) / BM;
-  const int ntiles = p.Cout / BN;
-  dim3 grid(mtiles * ntiles, batch, phases);
+  dim3 grid(mtiles * (p.Cout / BN), batch, phases);
   hipLaunchKernelGGL((conv_gemm_f32<BM, BN, WM, WN, ARGMIN>), grid, dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
+template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN>
+static hipError_t launch_x6w8(const ConvParams& p, int batch, int phases, hipStream_t s) {
+  const int mtiles = (p.Lq + BM - 1) / BM;
+  dim3 grid(mtiles * (p.Cout / BN), batch, phases);
+  hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, WM, WN, HALO, ARGMIN>), grid, dim3(512), 0, s, p);
+  return hipGetLastError();
+}
+
+static int tap_span(const ConvParams& p) { return (p.taps - 1) * (p.in_step < 0 ? -p.in_step : p.in_step); }
+
 hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
   if (p.Cin % BK || p.Cout % 32 || phases < 1 || phases > kMaxPhases) return hipErrorInvalidValue;
+  if (p.w6) {
+    const int span = tap_span(p);
+    if (span > 64) return hipErrorInvalidValue;
+    const bool h = span > 0;
+    if (p.Cout % 128 == 0) {
+      if (kname) *kname = h ? "conv_gemm_x6w8<256,128,halo>" : "conv_gemm_x6w8<256,128>";
+      return h ? launch_x6w8<256, 128, 4, 2, 64, false>(p, batch, phases, s)
+               : launch_x6w8<256, 128, 4, 2, 0, false>(p, batch, phases, s);
+    }
+    if (p.Cout % 64 == 0) {
+      if (kname) *kname = h ? "conv_gemm_x6w8<512,64,halo>" : "conv_gemm_x6w8<512,64>";
+      return h ? launch_x6w8<512, 64, 8, 1, 64, false>(p, batch, phases, s)
+               : launch_x6w8<512, 64, 8, 1, 0, false>(p, batch, phases, s);
+    }
+    if (kname) *kname = h ? "conv_gemm_x6w8<512,32,halo>" : "conv_gemm_x6w8<512,32>";
+    return h ? launch_x6w8<512, 32, 8, 1, 64, false>(p, batch, phases, s)
+             : launch_x6w8<512, 32, 8, 1, 0, false>(p, batch, phases, s);
+  }
   if (p.Cout % 128 == 0) {
     if (kname) *kname = "conv_gemm_f32<128,128>";
-    return launch_tile<128, 128, 2, 2, false>(p, batch, phases, s);
+    return launch_f32<128, 128, 2, 2, false>(p, batch, phases, s);
   }
   if (p.Cout % 64 == 0) {
     if (kname) *kname = "conv_gemm_f32<256,64>";
-    return launch_tile<256, 64, 4, 1, false>(p, batch, phases, s);
+    return launch_f32<256, 64, 4, 1, false>(p, batch, phases, s);
   }
   if (kname) *kname = "conv_gemm_f32<256,32>";
-  return launch_tile<256, 32, 4, 1, false>(p, batch, phases, s);
+  return launch_f32<256, 32, 4, 1, false>(p, batch, phases, s);
 }
 
 int vq_argmin_ntiles(int ncodes) { return ncodes / 128; }
 
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname) {
   if (p.Cin % BK || p.Cout % 128) return hipErrorInvalidValue;
-  if (kname) *kname = "vq_dist_argmin_f32<128,128>";
   ConvParams q = p;
   q.Lq = rows;
   q.Lin = rows;
-  return launch_tile<128, 128, 2, 2, true>(q, 1, 1, s);
+  if (p.w6) {
+    if (kname) *kname = "vq_dist_argmin_x6w8<256,128>";
+    return launch_x6w8<256, 128, 4, 2, 0, true>(q, 1, 1, s);
+  }
+  if (kname) *kname = "vq_dist_argmin_f32<128,128>";
+  return launch_f32<128, 128, 2, 2, true>(q, 1, 1, s);
 }
 
 }  // namespace dcx

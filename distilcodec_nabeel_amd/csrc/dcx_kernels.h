@@ -25,7 +25,8 @@ constexpr int kMaxPhases = 8;
 // Rows of x outside [0, Lin) read as zero (zero padding).  Channels-last everywhere.
 struct ConvParams {
   const float* x;
-  const float* w;
+  const float* w;               // fp32 weights [phase][Cout][taps*Cin]
+  const unsigned short* w6;     // if set: x6 mode, bf16 split weights [phase][tap][Cin/16][Cout][2][3][8]
   const float* bias;   // may be null
   const float* gamma;  // EPI_GAMMA_RES
   const float* res;    // EPI_GAMMA_RES / EPI_RES, layout of y

@@ -6,6 +6,7 @@ pointers to the C ABI.  Tensors are channels-last ([B][T][C]) as the kernels pro
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -14,8 +15,14 @@ from . import _native
 from .config import check_supported
 
 
+GEMM_MODES = {"f32": _native.DCX_GEMM_F32, "x6": _native.DCX_GEMM_X6}
+
+
 class NativeCodec:
-    def __init__(self, cfg: dict, state: dict, device, with_generator: bool = True):
+    """`gemm`: "x6" (default; fp32 operands as three bf16 planes, six exact products, fp32
+    accumulation) or "f32" (v_mfma_f32_32x32x2_f32).  Env DCX_GEMM overrides the default."""
+
+    def __init__(self, cfg: dict, state: dict, device, with_generator: bool = True, gemm: str | None = None):
         check_supported(cfg)
         self.cfg = cfg
         self.device = torch.device(device)
@@ -36,6 +43,10 @@ class NativeCodec:
         with torch.cuda.device(self.device):
             self._check(self.L.dcx_create(ctypes.byref(self.c), ctypes.byref(h)), None)
             self.h = h
+            self.gemm = gemm or os.environ.get("DCX_GEMM", "x6")
+            if self.gemm not in GEMM_MODES:
+                raise ValueError(f"unknown GEMM mode {self.gemm!r}; expected one of {sorted(GEMM_MODES)}")
+            self._check(self.L.dcx_set_gemm_mode(self.h, GEMM_MODES[self.gemm]))
             for part in ("encoder", "quantizer") + (("generator",) if with_generator else ()):
                 for k, v in state[part].items():
                     a = np.ascontiguousarray(np.asarray(v, dtype=np.float32))
@@ -87,6 +98,10 @@ class NativeCodec:
         if t.device != self.device or t.dtype != dtype or not t.is_contiguous():
             t = t.to(device=self.device, dtype=dtype).contiguous()
         return t
+
+    def set_gemm(self, mode: str) -> None:
+        self._check(self.L.dcx_set_gemm_mode(self.h, GEMM_MODES[mode]))
+        self.gemm = mode
 
     def num_frames(self, n_samples: int) -> int:
         return int(self.L.dcx_num_frames(self.h, n_samples))
@@ -189,3 +204,45 @@ class NativeCodec:
                                                 ctypes.byref(fl), ctypes.byref(by)))
             out[name.value.decode()] = {"launches": launches.value, "ms": ms.value, "flops": fl.value, "bytes": by.value}
         return out
+
+
+class NativeConv:
+    """The conv primitive of libdcx (dcx_conv_*): Conv1d ("same" padding, dilation) or
+    ConvTranspose1d (padding (k-stride)/2) on channels-last fp32 tensors."""
+
+    def __init__(self, weight: np.ndarray, bias=None, dilation: int = 1, transposed: bool = False, stride: int = 1):
+        self.L = _native.lib()
+        w = np.ascontiguousarray(weight, dtype=np.float32)
+        if transposed:
+            self.cin, self.cout, self.k = w.shape
+        else:
+            self.cout, self.cin, self.k = w.shape
+        b = None if bias is None else np.ascontiguousarray(bias, dtype=np.float32)
+        self.stride = stride if transposed else 1
+        self._b = b
+        h = ctypes.c_void_p()
+        rc = self.L.dcx_conv_create(w.ctypes.data_as(ctypes.c_void_p), None if b is None else b.ctypes.data_as(ctypes.c_void_p),
+                                    self.cin, self.cout, self.k, dilation, 1 if transposed else 0, stride, ctypes.byref(h))
+        if rc != _native.DCX_OK:
+            raise ValueError(f"dcx_conv_create failed: {self.L.dcx_status_string(rc).decode()}")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            self.L.dcx_conv_destroy(h)
+            self.h = None
+
+    def __call__(self, x: torch.Tensor, gemm: str = "x6", epi: int = 0, res: torch.Tensor | None = None,
+                 want_y: bool = True, want_silu: bool = False):
+        B, Lin, C = x.shape
+        assert C == self.cin and x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()
+        Lout = Lin * self.stride
+        y = torch.empty(B, Lout, self.cout, device=x.device) if want_y else None
+        ys = torch.empty(B, Lout, self.cout, device=x.device) if want_silu else None
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        rc = self.L.dcx_conv_forward(self.h, GEMM_MODES[gemm], ptr(x), B, Lin, ptr(y), ptr(ys), ptr(res), epi,
+                                     ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+        if rc != _native.DCX_OK:
+            raise _native.NativeError(rc, "dcx_conv_forward failed")
+        return (y, ys) if want_silu else y

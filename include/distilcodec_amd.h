@@ -126,6 +126,29 @@ int dcx_encode_decode(dcx_codec* h, const float* audio, int32_t batch, int64_t n
 /* Batched 2-D transpose [B][R][C] -> [B][C][R] (channels-first <-> channels-last bridge). */
 int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int64_t cols, void* stream);
 
+/* Arithmetic of every contraction (convs, linears, STFT, mel, VQ distances):
+ *  DCX_GEMM_X6  (default) fp32 operands split into three bf16 planes, six exact bf16 products per
+ *               fp32 product, fp32 accumulation on v_mfma_f32_32x32x16_bf16 (fp32-level accuracy);
+ *  DCX_GEMM_F32 v_mfma_f32_32x32x2_f32 (IEEE fp32 fma chain).
+ * May be changed at any time; the VQ decode table keeps the mode active at dcx_finalize. */
+#define DCX_GEMM_F32 0
+#define DCX_GEMM_X6 1
+int dcx_set_gemm_mode(dcx_codec* h, int32_t mode);
+int32_t dcx_get_gemm_mode(const dcx_codec* h);
+
+/* Standalone 1-D convolution primitive (the kernel family behind every stage), for tests and
+ * benchmarks.  weight: host fp32, Conv1d layout [Cout][Cin][k] (transposed=0) or
+ * ConvTranspose1d layout [Cin][Cout][k] (transposed=1, padding (k-stride)/2); bias may be NULL.
+ * dcx_conv_forward: x [B][Lin][Cin] -> y [B][Lout][Cout] (channels-last, Lout = Lin for a conv
+ * with "same" padding, stride*Lin for the transposed form) with epilogue `epi`
+ * (0 bias, 1 gelu, 3 residual add: y = res + v), optional second output y_silu = silu(v). */
+typedef struct dcx_conv dcx_conv;
+int dcx_conv_create(const float* weight, const float* bias, int32_t cin, int32_t cout, int32_t k, int32_t dilation,
+                    int32_t transposed, int32_t stride, dcx_conv** out);
+int dcx_conv_forward(dcx_conv* c, int32_t gemm_mode, const float* x, int32_t batch, int64_t lin, float* y,
+                     float* y_silu, const float* res, int32_t epi, void* stream);
+void dcx_conv_destroy(dcx_conv* c);
+
 /* Optional per-kernel timing: when enabled, every launch is bracketed by HIP events on its
  * stream.  dcx_profile_read synchronises the device and returns, per kernel symbol, the
  * launch count, summed device milliseconds and summed algorithmic FLOPs / bytes. */

@@ -25,11 +25,11 @@ def _snr(x, ref):
     return 10 * np.log10((ref ** 2).sum() / max(((x - ref) ** 2).sum(), 1e-300))
 
 
-@pytest.fixture(scope="module")
-def eng(cfg, state):
+@pytest.fixture(scope="module", params=["x6", "f32"])
+def eng(cfg, state, request):
     from distilcodec_nabeel_amd.engine import NativeCodec
 
-    return NativeCodec(cfg, state, "cuda:0")
+    return NativeCodec(cfg, state, "cuda:0", gemm=request.param)
 
 
 def _decisive(g):
