@@ -72,6 +72,7 @@ struct Bump {  // workspace carve-out, 256-byte aligned
   Bump(void* p, size_t c, bool d) : base((char*)p), cap(c), dry(d) {}
   float* f(size_t n) { return (float*)raw(n * sizeof(float)); }
   int* i(size_t n) { return (int*)raw(n * sizeof(int)); }
+  unsigned short* u16(size_t n) { return (unsigned short*)raw(n * sizeof(unsigned short)); }
   void* raw(size_t bytes) {
     size_t o = (off + 255) & ~(size_t)255;
     off = o + bytes;
@@ -101,6 +102,7 @@ struct dcx_codec {
   BlockW vq_down_blk, vq_up_blk;
   float *codebook = nullptr, *e2 = nullptr, *ptable = nullptr;
   unsigned short* codebook6 = nullptr;
+  unsigned short* ptable6 = nullptr;  // decode table as activation planes (x6 mode gathers)
   int gemm_mode = DCX_GEMM_X6;
 
   ConvW conv_pre;
@@ -462,34 +464,64 @@ int max_gen_width(const dcx_config& c) {  // max over generator layers of channe
 // ----------------------------------------------------------------------------------------
 // launches
 // ----------------------------------------------------------------------------------------
+// An activation tensor [rows][C]: fp32 and/or x6 planes ([rows][C/8][3][8] bf16, dcx_planes.h).
+struct Act {
+  float* f = nullptr;
+  unsigned short* p = nullptr;
+};
+struct CAct {
+  const float* f = nullptr;
+  const unsigned short* p = nullptr;
+  CAct() = default;
+  CAct(const float* f_, const unsigned short* p_) : f(f_), p(p_) {}
+  CAct(const Act& a) : f(a.f), p(a.p) {}
+};
+
+bool x6_mode(const dcx_codec* h) { return h->gemm_mode == DCX_GEMM_X6; }
+
+// Workspace for a tensor consumed only by convs: planes in x6 mode, fp32 otherwise.
+Act conv_input(dcx_codec* h, Bump& ws, size_t n) {
+  Act a;
+  if (x6_mode(h)) a.p = ws.u16(3 * n);
+  else a.f = ws.f(n);
+  return a;
+}
+
 struct ConvCall {
-  const float* x;
+  CAct x;
   long long x_bstride;
   int batch, Lin, Lq, ldx;
-  float* y = nullptr;
-  float* y2 = nullptr;
+  float* y = nullptr;            // v
+  float* y2 = nullptr;           // silu(v), fp32
+  unsigned short* y6 = nullptr;  // planes of v
+  unsigned short* y6s = nullptr; // planes of silu(v)
   float* macc = nullptr;
   const float* res = nullptr;
   const float* gamma = nullptr;
-  long long y_bstride = 0;
-  int ldy = 0;
   int epi = dcx::EPI_BIAS, mean = dcx::MEAN_NONE;
+  void silu_to(const Act& a) { y2 = a.f; y6s = a.p; }
+  void out_to(const Act& a) { y = a.f; y6 = a.p; }
 };
 
-int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s) {
+int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, bool force_f32 = false) {
+  const bool x6 = x6_mode(h) && !force_f32;
+  if (x6 ? (!c.x.p || !w.w6) : !c.x.f) return fail(h, DCX_ERR_STATE, "internal: conv input missing for GEMM mode");
   ConvParams p{};
-  p.x = c.x;
+  p.x = c.x.f;
+  p.x6 = x6 ? c.x.p : nullptr;
   p.w = w.w;
-  p.w6 = h->gemm_mode == DCX_GEMM_X6 ? w.w6 : nullptr;
+  p.w6 = x6 ? w.w6 : nullptr;
   p.bias = w.b;
   p.gamma = c.gamma;
   p.res = c.res;
   p.y = c.y;
   p.y2 = c.y2;
+  p.y6 = c.y6;
+  p.y6s = c.y6s;
   p.macc = c.macc;
   p.x_bstride = c.x_bstride;
-  p.ldy = c.ldy ? c.ldy : w.cout;
-  p.y_bstride = c.y_bstride ? c.y_bstride : (long long)c.Lq * w.out_mul * p.ldy;
+  p.ldy = w.cout;
+  p.y_bstride = (long long)c.Lq * w.out_mul * p.ldy;
   p.w_phase_stride = (long long)w.cout * w.taps * w.cin;
   p.Lin = c.Lin;
   p.Lq = c.Lq;
@@ -512,14 +544,23 @@ int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s) {
 }
 
 // Pointwise conv / Linear over all B*T rows at once.
-int run_pointwise(dcx_codec* h, const ConvW& w, const float* x, long long rows, float* y, hipStream_t s,
-                  int epi = dcx::EPI_BIAS, const float* res = nullptr, const float* gamma = nullptr) {
-  ConvCall c{x, 0, 1, (int)rows, (int)rows, 0};
-  c.y = y;
-  c.res = res;
-  c.gamma = gamma;
-  c.epi = epi;
-  return run_conv(h, w, c, s);
+ConvCall pointwise(CAct x, long long rows) {
+  ConvCall c;
+  c.x = x;
+  c.x_bstride = 0;
+  c.batch = 1;
+  c.Lin = c.Lq = (int)rows;
+  c.ldx = 0;
+  return c;
+}
+ConvCall framed(CAct x, int B, int L, int C) {
+  ConvCall c;
+  c.x = x;
+  c.x_bstride = (long long)L * C;
+  c.batch = B;
+  c.Lin = c.Lq = L;
+  c.ldx = C;
+  return c;
 }
 
 #define RUN(expr)             \
@@ -535,92 +576,132 @@ int run_pointwise(dcx_codec* h, const ConvW& w, const float* x, long long rows, 
     ps_.done(name, flops, bytes);              \
   } while (0)
 
-// ConvNeXtBlock in place on x [B][T][C]; ln: [M][C] scratch, hid: [M][4C] scratch.
-int run_block(dcx_codec* h, const BlockW& bw, float* x, int B, int T, float* ln, float* hid, hipStream_t s) {
-  const long long M = (long long)B * T;
-  const int C = bw.C;
-  LAUNCH(h, s, "dwconv_ln", 14.0 * M * C, 8.0 * M * C,
-         dcx::launch_dwconv_ln(x, ln, bw.dww, bw.dwb, bw.ln.w, bw.ln.b, B, T, C, s));
-  RUN(run_pointwise(h, bw.pw1, ln, M, hid, s, dcx::EPI_GELU));
-  RUN(run_pointwise(h, bw.pw2, hid, M, x, s, dcx::EPI_GAMMA_RES, x, bw.gamma));
+// fp32 -> planes for a tensor handed in by the caller (x6 mode only).
+int ensure_planes(dcx_codec* h, CAct& a, long long rows, int C, Bump& ws, hipStream_t s) {
+  if (!x6_mode(h) || a.p) return DCX_OK;
+  unsigned short* p = ws.u16((size_t)rows * C * 3);
+  if (ws.dry) return DCX_OK;
+  if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small");
+  LAUNCH(h, s, "split_planes", 0, 10.0 * rows * C, dcx::launch_split_planes(a.f, p, rows, C, s));
+  a.p = p;
   return DCX_OK;
 }
 
-int run_ln(dcx_codec* h, const LnW& l, const float* x, float* y, long long rows, hipStream_t s) {
+// ConvNeXtBlock in place on x [B][T][C] (fp32 residual stream); out6: optional planes of the
+// block output for a following conv.  ln: [M][C], hid: [M][4C] conv-input scratch.
+int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, int B, int T, Act ln, Act hid,
+              hipStream_t s) {
+  const long long M = (long long)B * T;
+  const int C = bw.C;
+  LAUNCH(h, s, "dwconv_ln", 14.0 * M * C, 8.0 * M * C,
+         dcx::launch_dwconv_ln(x, ln.f, ln.p, bw.dww, bw.dwb, bw.ln.w, bw.ln.b, B, T, C, s));
+  ConvCall c1 = pointwise(ln, M);
+  c1.out_to(hid);
+  c1.epi = dcx::EPI_GELU;
+  RUN(run_conv(h, bw.pw1, c1, s));
+  ConvCall c2 = pointwise(hid, M);
+  c2.y = x;
+  c2.y6 = out6;
+  c2.res = x;
+  c2.gamma = bw.gamma;
+  c2.epi = dcx::EPI_GAMMA_RES;
+  RUN(run_conv(h, bw.pw2, c2, s));
+  return DCX_OK;
+}
+
+int run_ln(dcx_codec* h, const LnW& l, const float* x, Act y, long long rows, hipStream_t s) {
   LAUNCH(h, s, "ln_rows", 8.0 * rows * l.C, 8.0 * rows * l.C,
-         dcx::launch_ln_rows(x, y, l.w, l.b, rows, l.C, 1e-6f, 1, s));
+         dcx::launch_ln_rows(x, y.f, y.p, l.w, l.b, rows, l.C, 1e-6f, 1, s));
   return DCX_OK;
 }
 
 // ---------------- stage bodies (dry=true only sizes the workspace) ----------------
-int stage_mel(dcx_codec* h, const float* audio, int B, int64_t n, float* mel, Bump& ws, hipStream_t s) {
+int stage_mel(dcx_codec* h, const float* audio, int B, int64_t n, Act mel, Bump& ws, hipStream_t s) {
   const dcx_config& c = h->cfg;
   const int T = (int)frames_of(c, n);
   const int rows = T + c.n_fft / c.hop - 1;
-  float* fr = ws.f((size_t)B * rows * c.hop);
+  Act fr = conv_input(h, ws, (size_t)B * rows * c.hop);
   float* spec = ws.f((size_t)B * T * h->dft.cout);
-  float* mag = ws.f((size_t)B * T * h->melfb.cin);
+  Act mag = conv_input(h, ws, (size_t)B * T * h->melfb.cin);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for mel");
   LAUNCH(h, s, "frame_pad", 0, 8.0 * B * rows * c.hop,
-         dcx::launch_frame_pad(audio, fr, B, n, rows, c.hop, (c.win - c.hop) / 2, s));
-  ConvCall cc{fr, (long long)rows * c.hop, B, rows, T, c.hop};
+         dcx::launch_frame_pad(audio, fr.f, fr.p, B, n, rows, c.hop, (c.win - c.hop) / 2, s));
+  ConvCall cc = framed(fr, B, rows, c.hop);
+  cc.Lq = T;
   cc.y = spec;
   RUN(run_conv(h, h->dft, cc, s));
   const int nbins = c.n_fft / 2 + 1;
   LAUNCH(h, s, "spec_mag", 4.0 * B * T * nbins, 4.0 * B * T * (h->dft.cout + h->melfb.cin),
-         dcx::launch_spec_mag(spec, mag, (long long)B * T, nbins, h->melfb.cin, s));
-  RUN(run_pointwise(h, h->melfb, mag, (long long)B * T, mel, s, dcx::EPI_LOGCLAMP));
+         dcx::launch_spec_mag(spec, mag.f, mag.p, (long long)B * T, nbins, h->melfb.cin, s));
+  ConvCall cm = pointwise(mag, (long long)B * T);
+  cm.out_to(mel);
+  cm.epi = dcx::EPI_LOGCLAMP;
+  RUN(run_conv(h, h->melfb, cm, s));
   return DCX_OK;
 }
 
-int stage_encode(dcx_codec* h, const float* mel, int B, int T, float* feat, Bump& ws, hipStream_t s) {
+int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipStream_t s) {
   const dcx_config& c = h->cfg;
   const long long M = (long long)B * T;
   const int cmax = c.enc_dims[3];
+  RUN(ensure_planes(h, mel, M, c.n_mels, ws, s));
   float* xa = ws.f((size_t)M * cmax);
   float* xb = ws.f((size_t)M * cmax);
-  float* hid = ws.f((size_t)M * 4 * cmax);
+  Act ln = conv_input(h, ws, (size_t)M * cmax);
+  Act hid = conv_input(h, ws, (size_t)M * 4 * cmax);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for encode");
-  ConvCall cc{mel, (long long)T * c.n_mels, B, T, T, c.n_mels};
+  ConvCall cc = framed(mel, B, T, c.n_mels);
   cc.y = xa;
   RUN(run_conv(h, h->stem, cc, s));
-  RUN(run_ln(h, h->stem_ln, xa, xb, M, s));
+  RUN(run_ln(h, h->stem_ln, xa, Act{xb, nullptr}, M, s));
   for (int i = 0; i < 4; ++i) {
     if (i > 0) {
-      RUN(run_ln(h, h->ds_ln[i], xb, xa, M, s));
-      RUN(run_pointwise(h, h->ds_conv[i], xa, M, xb, s));
+      RUN(run_ln(h, h->ds_ln[i], xb, ln, M, s));
+      ConvCall cd = pointwise(ln, M);
+      cd.y = xb;
+      RUN(run_conv(h, h->ds_conv[i], cd, s));
     }
-    for (auto& bw : h->blocks[i]) RUN(run_block(h, bw, xb, B, T, xa, hid, s));
+    for (auto& bw : h->blocks[i]) RUN(run_block(h, bw, xb, nullptr, B, T, ln, hid, s));
   }
   RUN(run_ln(h, h->enc_norm, xb, feat, M, s));
   return DCX_OK;
 }
 
-int stage_vq_encode(dcx_codec* h, const float* feat, int B, int T, int32_t* codes, float* pin, float* fup,
-                    float* quant, Bump& ws, hipStream_t s) {
+int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float* pin, float* fup, float* quant,
+                    Bump& ws, hipStream_t s) {
   const dcx_config& c = h->cfg;
   const long long M = (long long)B * T;
   const int D = c.vq_dim, CD = c.codebook_dim, NC = c.codebook_size;
   const int ntiles = dcx::vq_argmin_ntiles(NC);
-  float* x = ws.f((size_t)M * D);
-  float* ln = ws.f((size_t)M * D);
-  float* hid = ws.f((size_t)M * 4 * D);
+  const bool x6 = x6_mode(h);
+  RUN(ensure_planes(h, feat, M, D, ws, s));
+  float* X = ws.f((size_t)M * D);
+  unsigned short* X6 = x6 ? ws.u16((size_t)M * D * 3) : nullptr;
+  Act ln = conv_input(h, ws, (size_t)M * D);
+  Act hid = conv_input(h, ws, (size_t)M * 4 * D);
   float* P = pin ? pin : ws.f((size_t)M * CD);
+  unsigned short* P6 = x6 ? ws.u16((size_t)M * CD * 3) : nullptr;
   float* x2 = ws.f((size_t)M);
   float* pv = ws.f((size_t)M * ntiles);
   int* pi = ws.i((size_t)M * ntiles);
-  float* zd = ws.f((size_t)M * D);
+  Act zd = conv_input(h, ws, (size_t)M * D);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for vq_encode");
-  RUN(run_pointwise(h, h->vq_down, feat, M, x, s));
-  RUN(run_block(h, h->vq_down_blk, x, B, T, ln, hid, s));
-  RUN(run_pointwise(h, h->vq_pin, x, M, P, s));
+  ConvCall cd = pointwise(feat, M);
+  cd.y = X;
+  RUN(run_conv(h, h->vq_down, cd, s));
+  RUN(run_block(h, h->vq_down_blk, X, X6, B, T, ln, hid, s));
+  ConvCall cp = pointwise(CAct(X, X6), M);
+  cp.y = P;
+  cp.y6 = P6;
+  RUN(run_conv(h, h->vq_pin, cp, s));
   LAUNCH(h, s, "row_sqnorm", 2.0 * M * CD, 4.0 * M * CD, dcx::launch_row_sqnorm(P, M, CD, x2, s));
   {
     ConvParams p{};
-    p.x = P; p.w = h->codebook; p.w6 = h->gemm_mode == DCX_GEMM_X6 ? h->codebook6 : nullptr; p.Cin = CD; p.Cout = NC; p.ldx = CD; p.taps = 1; p.in_step = 1; p.out_mul = 1;
+    p.x = P; p.x6 = P6; p.w = h->codebook; p.w6 = x6 ? h->codebook6 : nullptr;
+    p.Cin = CD; p.Cout = NC; p.ldx = CD; p.taps = 1; p.in_step = 1; p.out_mul = 1;
     p.x2 = x2; p.e2 = h->e2; p.part_val = pv; p.part_idx = pi;
     ProfScope ps(h, s);
     const char* kname = "vq";
@@ -630,75 +711,96 @@ int stage_vq_encode(dcx_codec* h, const float* feat, int B, int T, int32_t* code
   LAUNCH(h, s, "vq_reduce", 0, 8.0 * M * ntiles, dcx::launch_vq_reduce(pv, pi, (int)M, ntiles, codes, s));
   if (fup) LAUNCH(h, s, "gather_rows", 0, 8.0 * M * CD, dcx::launch_gather_rows(h->codebook, NC, codes, M, CD, fup, nullptr, s));
   if (quant) {
-    LAUNCH(h, s, "gather_rows", 0, 8.0 * M * D, dcx::launch_gather_rows(h->ptable, NC, codes, M, D, zd, nullptr, s));
-    RUN(run_pointwise(h, h->vq_up, zd, M, quant, s));
-    RUN(run_block(h, h->vq_up_blk, quant, B, T, ln, hid, s));
+    if (x6)
+      LAUNCH(h, s, "gather_rows", 0, 12.0 * M * D,
+             dcx::launch_gather_rows((const float*)h->ptable6, NC, codes, M, D * 3 / 2, (float*)zd.p, nullptr, s));
+    else
+      LAUNCH(h, s, "gather_rows", 0, 8.0 * M * D, dcx::launch_gather_rows(h->ptable, NC, codes, M, D, zd.f, nullptr, s));
+    ConvCall cu = pointwise(zd, M);
+    cu.y = quant;
+    RUN(run_conv(h, h->vq_up, cu, s));
+    RUN(run_block(h, h->vq_up_blk, quant, nullptr, B, T, ln, hid, s));
   }
   return DCX_OK;
 }
 
-int stage_vq_decode(dcx_codec* h, const int32_t* codes, int B, int T, float* z, int32_t* n_invalid, Bump& ws,
+// z.f is required (fp32 residual stream of the up-path block); z.p optionally receives planes.
+int stage_vq_decode(dcx_codec* h, const int32_t* codes, int B, int T, Act z, int32_t* n_invalid, Bump& ws,
                     hipStream_t s) {
   const dcx_config& c = h->cfg;
   const long long M = (long long)B * T;
   const int D = c.vq_dim;
-  float* zd = ws.f((size_t)M * D);
-  float* ln = ws.f((size_t)M * D);
-  float* hid = ws.f((size_t)M * 4 * D);
+  Act zd = conv_input(h, ws, (size_t)M * D);
+  Act ln = conv_input(h, ws, (size_t)M * D);
+  Act hid = conv_input(h, ws, (size_t)M * 4 * D);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for vq_decode");
-  LAUNCH(h, s, "gather_rows", 0, 8.0 * M * D,
-         dcx::launch_gather_rows(h->ptable, c.codebook_size, codes, M, D, zd, n_invalid, s));
-  RUN(run_pointwise(h, h->vq_up, zd, M, z, s));
-  RUN(run_block(h, h->vq_up_blk, z, B, T, ln, hid, s));
+  if (x6_mode(h))
+    LAUNCH(h, s, "gather_rows", 0, 12.0 * M * D,
+           dcx::launch_gather_rows((const float*)h->ptable6, c.codebook_size, codes, M, D * 3 / 2, (float*)zd.p,
+                                   n_invalid, s));
+  else
+    LAUNCH(h, s, "gather_rows", 0, 8.0 * M * D,
+           dcx::launch_gather_rows(h->ptable, c.codebook_size, codes, M, D, zd.f, n_invalid, s));
+  ConvCall cu = pointwise(zd, M);
+  cu.y = z.f;
+  RUN(run_conv(h, h->vq_up, cu, s));
+  RUN(run_block(h, h->vq_up_blk, z.f, z.p, B, T, ln, hid, s));
   return DCX_OK;
 }
 
-int stage_generate(dcx_codec* h, const float* z, int B, int T, float* wav, Bump& ws, hipStream_t s) {
+int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hipStream_t s) {
   const dcx_config& c = h->cfg;
+  RUN(ensure_planes(h, z, (long long)B * T, c.vq_dim, ws, s));
   const size_t per = (size_t)B * T * max_gen_width(c);
-  float* S = ws.f(per);
-  float* X = ws.f(per);
-  float* XS = ws.f(per);
-  float* R = ws.f(per);
-  float* RS = ws.f(per);
-  float* Tb = ws.f(per);
+  float* X = ws.f(per);   // ConvT output (residual of each ResBlock's first pair)
+  float* R = ws.f(per);   // ResBlock state
+  float* Mx = ws.f(per);  // ParallelBlock mean accumulator; silu(mean) of the last stage
+  Act S = conv_input(h, ws, per);   // silu(stage input) -> ConvT
+  Act XS = conv_input(h, ws, per);  // silu(X)
+  Act RS = conv_input(h, ws, per);  // silu(R)
+  Act Tb = conv_input(h, ws, per);  // silu(c1 output)
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for generate");
   int C = c.gen_channels, L = T;
   {  // conv_pre, then the first stage's SiLU (generators.py:121,125) fused as the only output
-    ConvCall cc{z, (long long)T * c.vq_dim, B, T, T, c.vq_dim};
-    cc.y2 = S;
+    ConvCall cc = framed(z, B, T, c.vq_dim);
+    cc.silu_to(S);
     RUN(run_conv(h, h->conv_pre, cc, s));
   }
   for (int i = 0; i < c.n_ups; ++i) {
     const ConvW& up = h->ups[i];
     const int Co = up.cout, Lo = L * c.up_rates[i];
     {
-      ConvCall cc{S, (long long)L * C, B, L, L, C};
+      ConvCall cc = framed(S, B, L, C);
       cc.y = X;
-      cc.y2 = XS;
+      cc.silu_to(XS);
       RUN(run_conv(h, up, cc, s));
     }
+    const bool last_stage = i == c.n_ups - 1;
     for (int rb = 0; rb < c.n_res; ++rb) {
       for (int ci = 0; ci < 3; ++ci) {
-        const float* src = ci == 0 ? XS : RS;
+        const Act& src = ci == 0 ? XS : RS;
         const float* resid = ci == 0 ? X : R;
         {
-          ConvCall cc{src, (long long)Lo * Co, B, Lo, Lo, Co};
-          cc.y2 = Tb;
+          ConvCall cc = framed(src, B, Lo, Co);
+          cc.silu_to(Tb);
           RUN(run_conv(h, h->res[i][rb][ci][0], cc, s));
         }
-        ConvCall cc{Tb, (long long)Lo * Co, B, Lo, Lo, Co};
+        ConvCall cc = framed(Tb, B, Lo, Co);
         cc.epi = dcx::EPI_RES;
         cc.res = resid;
         if (ci < 2) {
           cc.y = R;
-          cc.y2 = RS;
+          cc.silu_to(RS);
         } else {
-          cc.macc = S;
+          cc.macc = Mx;
           cc.mean = rb == 0 ? dcx::MEAN_FIRST : (rb == c.n_res - 1 ? dcx::MEAN_LAST : dcx::MEAN_MID);
-          if (rb == c.n_res - 1) cc.y2 = S;  // silu(mean): consumed by ups[i+1] / conv_post
+          if (rb == c.n_res - 1) {
+            // silu(mean): input of ups[i+1], or (fp32, in place) of conv_post
+            if (last_stage) cc.y2 = Mx;
+            else cc.silu_to(S);
+          }
         }
         RUN(run_conv(h, h->res[i][rb][ci][1], cc, s));
       }
@@ -707,7 +809,7 @@ int stage_generate(dcx_codec* h, const float* z, int B, int T, float* wav, Bump&
     L = Lo;
   }
   LAUNCH(h, s, "conv_post_tanh", 2.0 * B * L * C * c.gen_post_k, 4.0 * B * L * (C + 1),
-         dcx::launch_conv_post_tanh(S, h->post_w, h->post_b, wav, B, L, C, c.gen_post_k, s));
+         dcx::launch_conv_post_tanh(Mx, h->post_w, h->post_b, wav, B, L, C, c.gen_post_k, s));
   return DCX_OK;
 }
 
@@ -716,9 +818,11 @@ int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int3
   const dcx_config& c = h->cfg;
   const int T = (int)frames_of(c, n);
   const long long M = (long long)B * T;
-  float* mel = ws.f((size_t)M * c.n_mels);
-  float* feat = ws.f((size_t)M * c.enc_dims[3]);
-  float* z = ws.f((size_t)M * c.vq_dim);
+  Act mel = conv_input(h, ws, (size_t)M * c.n_mels);
+  Act feat = conv_input(h, ws, (size_t)M * c.enc_dims[3]);
+  Act z;
+  z.f = ws.f((size_t)M * c.vq_dim);
+  if (x6_mode(h)) z.p = ws.u16((size_t)M * c.vq_dim * 3);
   const size_t mark = ws.off;
   size_t need = mark;
   auto sub = [&](auto fn) -> int {  // each sub-stage reuses the tail of the workspace
@@ -728,21 +832,13 @@ int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int3
     need = std::max(need, tail.off);
     return rc;
   };
-  if (ws.dry) {
-    sub([&](Bump& t) { return stage_mel(h, audio, B, n, mel, t, s); });
-    sub([&](Bump& t) { return stage_encode(h, mel, B, T, feat, t, s); });
-    sub([&](Bump& t) { return stage_vq_encode(h, feat, B, T, codes, nullptr, nullptr, nullptr, t, s); });
-    sub([&](Bump& t) { return stage_vq_decode(h, codes, B, T, z, nullptr, t, s); });
-    sub([&](Bump& t) { return stage_generate(h, z, B, T, wav, t, s); });
-    ws.off = need;
-    return DCX_OK;
-  }
-  if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for encode_decode");
+  if (!ws.dry && !ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for encode_decode");
   RUN(sub([&](Bump& t) { return stage_mel(h, audio, B, n, mel, t, s); }));
-  RUN(sub([&](Bump& t) { return stage_encode(h, mel, B, T, feat, t, s); }));
-  RUN(sub([&](Bump& t) { return stage_vq_encode(h, feat, B, T, codes, nullptr, nullptr, nullptr, t, s); }));
+  RUN(sub([&](Bump& t) { return stage_encode(h, CAct(mel), B, T, feat, t, s); }));
+  RUN(sub([&](Bump& t) { return stage_vq_encode(h, CAct(feat), B, T, codes, nullptr, nullptr, nullptr, t, s); }));
   RUN(sub([&](Bump& t) { return stage_vq_decode(h, codes, B, T, z, nullptr, t, s); }));
-  RUN(sub([&](Bump& t) { return stage_generate(h, z, B, T, wav, t, s); }));
+  RUN(sub([&](Bump& t) { return stage_generate(h, CAct(z), B, T, wav, t, s); }));
+  if (ws.dry) ws.off = need;
   return DCX_OK;
 }
 
@@ -912,10 +1008,16 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
     }
     // decode table: project_out applied to every code once, E * W_out^T + b_out
     h->ptable = B.alloc((size_t)NC * D);
+    h->ptable6 = (unsigned short*)B.alloc((size_t)NC * D * 3 / 2);
     if (!B.bad() && !B.dry) {
-      int rc = run_pointwise(h, pout, h->codebook, NC, h->ptable, 0);
+      // built once with the fp32 MFMA path (the codebook is not held as activation planes)
+      ConvCall cp = pointwise(CAct(h->codebook, nullptr), NC);
+      cp.y = h->ptable;
+      int rc = run_conv(h, pout, cp, 0, /*force_f32=*/true);
       if (rc != DCX_OK) return rc;
-      if (hipDeviceSynchronize() != hipSuccess) return fail(h, DCX_ERR_HIP, "decode-table build failed");
+      if (dcx::launch_split_planes(h->ptable, h->ptable6, NC, D, 0) != hipSuccess ||
+          hipDeviceSynchronize() != hipSuccess)
+        return fail(h, DCX_ERR_HIP, "decode-table build failed");
     }
   }
   // ---- generator ------------------------------------------------------------------------
@@ -975,7 +1077,7 @@ size_t dcx_workspace_size(const dcx_codec* h, int32_t batch, int64_t frames) {
   stage_encode_decode(hh, nullptr, batch, n, nullptr, nullptr, d, 0);
   size_t need = d.off;
   Bump q(nullptr, 0, true);  // vq_encode with every optional output in the workspace
-  stage_vq_encode(hh, nullptr, batch, (int)frames, nullptr, nullptr, nullptr, nullptr, q, 0);
+  stage_vq_encode(hh, CAct(), batch, (int)frames, nullptr, nullptr, nullptr, nullptr, q, 0);
   need = std::max(need, q.off + (size_t)batch * frames * (h->cfg.codebook_dim + h->cfg.vq_dim) * 4 + 1024);
   return need + 4096;
 }
@@ -993,35 +1095,35 @@ int dcx_mel(dcx_codec* h, const float* audio, int32_t batch, int64_t n, float* m
   if (!audio || !mel) return fail(h, DCX_ERR_INVALID_ARG, "null buffer");
   if (n <= (h->cfg.win - h->cfg.hop) / 2 || frames_of(h->cfg, n) < 1)
     return fail(h, DCX_ERR_INVALID_ARG, "clip too short for the reflect pad / one STFT frame");
-  return stage_mel(h, audio, batch, n, mel, ws, s);
+  return stage_mel(h, audio, batch, n, Act{mel, nullptr}, ws, s);
 }
 
 int dcx_encode(dcx_codec* h, const float* mel, int32_t batch, int64_t frames, float* feat, void* workspace,
                size_t ws_bytes, void* stream) {
   STAGE_PRE(false);
   if (!mel || !feat || frames <= 0) return fail(h, DCX_ERR_INVALID_ARG, "bad arguments");
-  return stage_encode(h, mel, batch, (int)frames, feat, ws, s);
+  return stage_encode(h, CAct(mel, nullptr), batch, (int)frames, Act{feat, nullptr}, ws, s);
 }
 
 int dcx_vq_encode(dcx_codec* h, const float* feat, int32_t batch, int64_t frames, int32_t* codes, float* x_pjt_in,
                   float* quantized_fup, float* quantized, void* workspace, size_t ws_bytes, void* stream) {
   STAGE_PRE(false);
   if (!feat || !codes || frames <= 0) return fail(h, DCX_ERR_INVALID_ARG, "bad arguments");
-  return stage_vq_encode(h, feat, batch, (int)frames, codes, x_pjt_in, quantized_fup, quantized, ws, s);
+  return stage_vq_encode(h, CAct(feat, nullptr), batch, (int)frames, codes, x_pjt_in, quantized_fup, quantized, ws, s);
 }
 
 int dcx_vq_decode(dcx_codec* h, const int32_t* codes, int32_t batch, int64_t frames, float* z, int32_t* n_invalid,
                   void* workspace, size_t ws_bytes, void* stream) {
   STAGE_PRE(false);
   if (!codes || !z || frames <= 0) return fail(h, DCX_ERR_INVALID_ARG, "bad arguments");
-  return stage_vq_decode(h, codes, batch, (int)frames, z, n_invalid, ws, s);
+  return stage_vq_decode(h, codes, batch, (int)frames, Act{z, nullptr}, n_invalid, ws, s);
 }
 
 int dcx_generate(dcx_codec* h, const float* z, int32_t batch, int64_t frames, float* wav, void* workspace,
                  size_t ws_bytes, void* stream) {
   STAGE_PRE(true);
   if (!z || !wav || frames <= 0) return fail(h, DCX_ERR_INVALID_ARG, "bad arguments");
-  return stage_generate(h, z, batch, (int)frames, wav, ws, s);
+  return stage_generate(h, CAct(z, nullptr), batch, (int)frames, wav, ws, s);
 }
 
 int dcx_encode_decode(dcx_codec* h, const float* audio, int32_t batch, int64_t n, int32_t* codes, float* wav,
@@ -1052,6 +1154,8 @@ int32_t dcx_get_gemm_mode(const dcx_codec* h) { return h ? h->gemm_mode : -1; }
 struct dcx_conv {
   dcx_codec scratch;  // owns the device allocations and the last error
   ConvW w;
+  unsigned short* planes = nullptr;  // x6 input planes of the last call (grown on demand)
+  size_t planes_cap = 0;
 };
 
 extern "C" {
@@ -1093,16 +1197,31 @@ int dcx_conv_forward(dcx_conv* c, int32_t gemm_mode, const float* x, int32_t bat
   if (epi == dcx::EPI_RES && !res) return DCX_ERR_INVALID_ARG;
   dcx_codec* h = &c->scratch;
   h->gemm_mode = gemm_mode;
-  ConvCall cc{x, (long long)lin * c->w.cin, batch, (int)lin, (int)lin, c->w.cin};
+  hipStream_t s = (hipStream_t)stream;
+  CAct xa(x, nullptr);
+  if (gemm_mode == DCX_GEMM_X6) {
+    const size_t need = (size_t)batch * lin * c->w.cin * 3;
+    if (need > c->planes_cap) {
+      if (c->planes) hipFree(c->planes);
+      c->planes = nullptr;
+      c->planes_cap = 0;
+      if (hipMalloc(&c->planes, need * sizeof(unsigned short)) != hipSuccess) return DCX_ERR_OOM;
+      c->planes_cap = need;
+    }
+    if (dcx::launch_split_planes(x, c->planes, (long long)batch * lin, c->w.cin, s) != hipSuccess) return DCX_ERR_HIP;
+    xa.p = c->planes;
+  }
+  ConvCall cc = framed(xa, batch, (int)lin, c->w.cin);
   cc.y = y;
   cc.y2 = y_silu;
   cc.res = res;
   cc.epi = epi;
-  return run_conv(h, c->w, cc, (hipStream_t)stream);
+  return run_conv(h, c->w, cc, s);
 }
 
 void dcx_conv_destroy(dcx_conv* c) {
   if (!c) return;
+  if (c->planes) hipFree(c->planes);
   for (void* p : c->scratch.allocs) hipFree(p);
   delete c;
 }

@@ -17,8 +17,9 @@
 //    hi*hi + hi*mid + mid*hi + hi*lo + mid*mid + lo*hi, each exact in fp32 (8x8-bit
 //    significands), accumulated in fp32 by v_mfma_f32_32x32x16_bf16.  The dropped terms are
 //    <= 2^-24 relative, i.e. fp32 rounding level; the MFMA ceiling is 16/6 = 2.67x the fp32 one.
-//    Weights are split once at load; activations are split while being staged into LDS, and
-//    each staged input tile (with its tap halo) serves every tap of the conv.
+//    Weights are split once at load; activations arrive already split (every producer writes
+//    the planes, dcx_planes.h), so staging is a plain copy, and each staged input tile (with its
+//    tap halo) serves every tap of the conv.
 //
 // MFMA fragment maps (cdna_hip_programming.md §3): 32x32x2 f32: lane l supplies A[l&31][k=l>>5]
 // and B[k=l>>5][l&31]; 32x32x16 bf16: A[l&31][k=8(l>>5)+j], B[k=8(l>>5)+j][l&31], j<8;
@@ -26,6 +27,7 @@
 #include <type_traits>
 
 #include "dcx_kernels.h"
+#include "dcx_planes.h"
 
 namespace dcx {
 
@@ -53,29 +55,94 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // Zero page read in place of out-of-range input rows (conv zero padding): selecting the address
 // instead of the loaded value keeps every staging load unconditional, so hipcc neither branches
 // around it nor waits vmcnt(0) after it (cdna_hip_programming.md §5, trap 4(c)).
-__device__ __attribute__((aligned(16))) float g_zero_row[BK] = {0.f};
+__device__ __attribute__((aligned(16))) float g_zero_row[32] = {0.f};
 
-// RNE fp32 -> bf16 bits (finite inputs) and back.
-__device__ __forceinline__ unsigned short bf16_bits(float x) {
-  const unsigned u = __float_as_uint(x);
-  return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
-}
-__device__ __forceinline__ float bf16_val(unsigned short b) { return __uint_as_float((unsigned)b << 16); }
-
-// x -> (hi, mid, lo) bf16 planes.
-__device__ __forceinline__ void split3(float x, unsigned short& h, unsigned short& m, unsigned short& l) {
-#ifdef DCX_EXP_NOSPLIT  // timing experiment only: wrong results
-  h = (unsigned short)(__float_as_uint(x) >> 16); m = h; l = h; return;
-#endif
-  h = bf16_bits(x);
-  const float r1 = x - bf16_val(h);
-  m = bf16_bits(r1);
-  const float r2 = r1 - bf16_val(m);
-  l = bf16_bits(r2);
+// ---------------------------------------------------------------------------------------------
+// Conv epilogue through LDS: the accumulator tile is written to LDS (in row passes that fit the
+// kernel's LDS), then each thread finishes 4 consecutive output channels of a row with 16-byte
+// loads of bias / gamma / residual / mean accumulator and 16-byte fp32 stores (8-byte plane
+// stores).  This keeps the per-element code out of the 64-way unrolled accumulator loop.
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, int LDS_FLOATS, int NT>
+__device__ __forceinline__ void epilogue_lds(const ConvParams& p, f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int q0,
+                                             int co0, int b, int ph, float* smem) {
+  constexpr int WR = BM / WM, WC = BN / WN;
+  constexpr int TM = WR / 32, TN = WC / 32;
+  constexpr int LDSW = BN + 4;
+  constexpr int RPP = (BM * LDSW <= LDS_FLOATS) ? BM
+                      : (BM / 2 * LDSW <= LDS_FLOATS) ? BM / 2
+                      : (BM / 4 * LDSW <= LDS_FLOATS) ? BM / 4 : WR;
+  static_assert(RPP % WR == 0 && RPP * LDSW <= LDS_FLOATS, "epilogue pass does not fit LDS");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lrow = lane & 31, rhalf = 4 * (lane >> 5);
+  const long long ob = (long long)b * p.y_bstride;
+  unsigned short* y6 = p.y6 ? p.y6 + ob * 3 : nullptr;
+  unsigned short* y6s = p.y6s ? p.y6s + ob * 3 : nullptr;
+#pragma unroll 1
+  for (int r0 = 0; r0 < BM; r0 += RPP) {
+    __syncthreads();
+    if (wm * WR >= r0 && wm * WR < r0 + RPP) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + rhalf - r0;
+            smem[row * LDSW + wn * WC + j * 32 + lrow] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int idx = tid; idx < RPP * (BN / 4); idx += NT) {
+      const int rl = idx / (BN / 4), c4 = (idx - rl * (BN / 4)) * 4;
+      const int q = q0 + r0 + rl;
+      if (q >= p.Lq) continue;
+      const int co = co0 + c4;
+      const long long orow = (long long)q * p.out_mul + ph;
+      const long long o = ob + orow * p.ldy + co;
+      f32x4 v = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + c4);
+      if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + co);
+      switch (p.epi) {
+        case EPI_GELU:
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
+          break;
+        case EPI_GAMMA_RES:
+          v = *reinterpret_cast<const f32x4*>(p.res + o) + *reinterpret_cast<const f32x4*>(p.gamma + co) * v;
+          break;
+        case EPI_RES: v = *reinterpret_cast<const f32x4*>(p.res + o) + v; break;
+        case EPI_LOGCLAMP:
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = logf(fmaxf(v[e], 1e-5f));
+          break;
+        default: break;
+      }
+      if (p.mean_mode == MEAN_FIRST) {
+        *reinterpret_cast<f32x4*>(p.macc + o) = v;
+        continue;
+      } else if (p.mean_mode == MEAN_MID) {
+        *reinterpret_cast<f32x4*>(p.macc + o) = *reinterpret_cast<const f32x4*>(p.macc + o) + v;
+        continue;
+      } else if (p.mean_mode == MEAN_LAST) {
+        v = (*reinterpret_cast<const f32x4*>(p.macc + o) + v) / 3.0f;
+      }
+      if (p.y) *reinterpret_cast<f32x4*>(p.y + o) = v;
+      if (y6) store_planes4(y6, orow, p.Cout, co, v[0], v[1], v[2], v[3]);
+      if (p.y2 || y6s) {
+        f32x4 sv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sv[e] = silu_f(v[e]);
+        if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
+        if (y6s) store_planes4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
-// Shared epilogue: per-element ops of the conv / argmin of the VQ search.
+// VQ search epilogue (registers): per-row argmin of the distance tile.
 // ---------------------------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, bool ARGMIN>
 __device__ __forceinline__ void epilogue(const ConvParams& p, f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int q0,
@@ -86,41 +153,8 @@ __device__ __forceinline__ void epilogue(const ConvParams& p, f32x16 (&acc)[BM /
   const int wm = wave / WN, wn = wave % WN;
   const int lrow = lane & 31;
   const int rhalf = 4 * (lane >> 5);
-  if constexpr (!ARGMIN) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int co = co0 + wn * WC + j * 32 + lrow;
-        const float bias = p.bias ? p.bias[co] : 0.f;
-        const float gam = (p.epi == EPI_GAMMA_RES) ? p.gamma[co] : 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int q = q0 + wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + rhalf;
-          if (q >= p.Lq) continue;
-          const long long o = (long long)b * p.y_bstride + (long long)(q * p.out_mul + ph) * p.ldy + co;
-          float v = acc[i][j][r] + bias;
-          switch (p.epi) {
-            case EPI_GELU: v = gelu_f(v); break;
-            case EPI_GAMMA_RES: v = p.res[o] + gam * v; break;
-            case EPI_RES: v = p.res[o] + v; break;
-            case EPI_LOGCLAMP: v = logf(fmaxf(v, 1e-5f)); break;
-            default: break;
-          }
-          if (p.mean_mode == MEAN_FIRST) {
-            p.macc[o] = v;
-            continue;
-          } else if (p.mean_mode == MEAN_MID) {
-            p.macc[o] = p.macc[o] + v;
-            continue;
-          } else if (p.mean_mode == MEAN_LAST) {
-            v = (p.macc[o] + v) / 3.0f;
-          }
-          if (p.y) p.y[o] = v;
-          if (p.y2) p.y2[o] = silu_f(v);
-        }
-      }
-  } else {
+  static_assert(ARGMIN, "register epilogue is the VQ search's; convs use epilogue_lds");
+  {
     // VQ search: dist = sqrt(clamp((|x|^2 + |e|^2) + (-2 x.e), 0)) exactly in the reference's
     // operation order (vector_quantize_pytorch.py:41-45); per row keep the smallest distance,
     // lowest code index on ties (torch argmax of -dist returns the first).
@@ -285,7 +319,10 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const ConvParams p) {
     if (kt + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
   }
-  epilogue<BM, BN, WM, WN, ARGMIN>(p, acc, q0, co0, nt, ntiles, b, ph, smem);
+  if constexpr (ARGMIN)
+    epilogue<BM, BN, WM, WN, true>(p, acc, q0, co0, nt, ntiles, b, ph, smem);
+  else
+    epilogue_lds<BM, BN, WM, WN, 2 * (BM + BN) * LDSK, 256>(p, acc, q0, co0, b, ph, smem);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -300,9 +337,9 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   constexpr int WR = BM / WM, WC = BN / WN;
   constexpr int TM = WR / 32, TN = WC / 32;
   constexpr int AROWS = BM + HALO;
-  constexpr int A_F4 = AROWS * 4;
+  constexpr int A_P = AROWS * 6;  // 16-byte pieces of a staged input tile (planes)
   constexpr int B_P = BN * 6;
-  constexpr int A_PT = (A_F4 + 511) / 512, B_PT = (B_P + 511) / 512;
+  constexpr int A_PT = (A_P + 511) / 512, B_PT = (B_P + 511) / 512;
   constexpr int ABUF = AROWS * XROW, BBUF = BN * XROW;
 
   // LDS: input tiles (2, by chunk parity) + weight-tile ring (3, by step mod 3).
@@ -315,7 +352,8 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
   const int b = blockIdx.y, ph = blockIdx.z;
-  const float* __restrict__ xb = p.x + (long long)b * p.x_bstride;
+  const unsigned short* __restrict__ xb6 = p.x6 + (long long)b * p.x_bstride * 3;
+  const long long ldx6 = (long long)p.ldx * 3;
   const int nchunks = p.Cin / BK;
   const int taps = p.taps;
   const int nsteps = nchunks * taps;
@@ -327,12 +365,12 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   const int lin = p.Lin;
 
   // Branch-free staging slots (surplus slots duplicate the last element).
-  int a_row[A_PT], a_col[A_PT];
+  int a_row[A_PT], a_k[A_PT];
 #pragma unroll
   for (int i = 0; i < A_PT; ++i) {
-    const int idx = min(tid + 512 * i, A_F4 - 1);
-    a_row[i] = idx >> 2;
-    a_col[i] = idx & 3;
+    const int idx = min(tid + 512 * i, A_P - 1);
+    a_row[i] = idx / 6;
+    a_k[i] = idx - a_row[i] * 6;
   }
   int b_off[B_PT], b_lds[B_PT];
 #pragma unroll
@@ -343,7 +381,10 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
     b_lds[i] = col * XROW + piece * 8;
   }
 
-  f32x4 ra[2][A_PT];
+  // With a tap halo (taps >= 2) at most one input-chunk load is in flight, so one register set
+  // suffices; 1-tap convs load a chunk every step and alternate two sets.
+  constexpr int RA_SETS = HALO > 0 ? 1 : 2;
+  f32x4 ra[RA_SETS][A_PT];
   f32x4 rb[2][B_PT];
 
   auto loadA = [&](int c, f32x4(&r)[A_PT]) {
@@ -351,26 +392,15 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
     for (int i = 0; i < A_PT; ++i) {
       const int ir = row0 + a_row[i];
       const bool ok = ir >= 0 && ir < lin;
-      const float* src = ok ? xb + (long long)ir * p.ldx + c * BK + a_col[i] * 4 : g_zero_row + a_col[i] * 4;
+      const unsigned short* src =
+          ok ? xb6 + (long long)ir * ldx6 + c * 48 + a_k[i] * 8 : reinterpret_cast<const unsigned short*>(g_zero_row);
       r[i] = *reinterpret_cast<const f32x4*>(src);
     }
   };
   auto storeA = [&](int buf, const f32x4(&r)[A_PT]) {
     unsigned short* A = lds + buf * ABUF;
 #pragma unroll
-    for (int i = 0; i < A_PT; ++i) {
-      s16x4 hv, mv, lv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        unsigned short h, m, l;
-        split3(r[i][e], h, m, l);
-        hv[e] = (short)h; mv[e] = (short)m; lv[e] = (short)l;
-      }
-      unsigned short* dst = A + a_row[i] * XROW + (a_col[i] >> 1) * 24 + (a_col[i] & 1) * 4;
-      *reinterpret_cast<s16x4*>(dst) = hv;
-      *reinterpret_cast<s16x4*>(dst + 8) = mv;
-      *reinterpret_cast<s16x4*>(dst + 16) = lv;
-    }
+    for (int i = 0; i < A_PT; ++i) *reinterpret_cast<f32x4*>(A + a_row[i] * XROW + a_k[i] * 8) = r[i];
   };
   auto loadB = [&](int c, int m, f32x4(&r)[B_PT]) {
     const unsigned short* src = wbase + ((long long)m * nchunks + c) * wslab;
@@ -437,7 +467,7 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   adv(c3, m3);
   // in flight for the first loop step: B(2) and the input chunk first used at step 2
   loadB(min(c2, nchunks - 1), c2 < nchunks ? m2 : taps - 1, rb[1]);
-  if (m2 == 0 && c2 < nchunks) loadA(c2, ra[1]);
+  if (m2 == 0 && c2 < nchunks) loadA(c2, ra[1 % RA_SETS]);
   __syncthreads();
   readF(0, 0, 0, af[0], bfr[0]);
 
@@ -449,7 +479,7 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
     if (s + 1 < nsteps) readF(c1, m1, slot1, af[1 - Q], bfr[1 - Q]);
     // 2. global loads for step s+3 (B) and for the input chunk first used at step s+3
     loadB(min(c3, nchunks - 1), c3 < nchunks ? m3 : taps - 1, rb[Q]);
-    if (m3 == 0 && c3 < nchunks) loadA(c3, ra[Q]);
+    if (m3 == 0 && c3 < nchunks) loadA(c3, ra[Q % RA_SETS]);
     // 3. MFMAs of step s
 #define DCX_MF(i, j, x, y) \
   acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[Q][i][x]), \
@@ -468,7 +498,7 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
 #undef DCX_MF
     // 4. stage step s+2: weight tile into its ring slot; its input chunk if s+2 opens one
     storeB(slot2, rb[1 - Q]);
-    if (m2 == 0 && c2 < nchunks) storeA(c2 & 1, ra[1 - Q]);
+    if (m2 == 0 && c2 < nchunks) storeA(c2 & 1, ra[(1 - Q) % RA_SETS]);
     __syncthreads();
     adv(c1, m1);
     adv(c2, m2);
@@ -480,7 +510,10 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
     step(s, std::integral_constant<int, 0>{});
     if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>{});
   }
-  epilogue<BM, BN, WM, WN, ARGMIN>(p, acc, q0, co0, nt, ntiles, b, ph, reinterpret_cast<float*>(lds));
+  if constexpr (ARGMIN)
+    epilogue<BM, BN, WM, WN, true>(p, acc, q0, co0, nt, ntiles, b, ph, reinterpret_cast<float*>(lds));
+  else
+    epilogue_lds<BM, BN, WM, WN, (2 * ABUF + 3 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -23,8 +23,11 @@ constexpr int kMaxPhases = 8;
 // out[b][q*out_mul + phase][co] = epi( sum_{m<taps} sum_{ci<Cin} x[b][q + in_base[phase] + m*in_step][ci]
 //                                       * w[phase][co][m*Cin + ci] + bias[co] )
 // Rows of x outside [0, Lin) read as zero (zero padding).  Channels-last everywhere.
+// x6 activations ("planes"): an fp32 tensor [rows][C] held as three bf16 planes interleaved per
+// 8 channels, [rows][C/8][plane 3][8] (6 bytes/element); hi + mid + lo reproduces x to 2^-27.
 struct ConvParams {
   const float* x;
+  const unsigned short* x6;     // x6 mode input planes (row stride 3*ldx elements)
   const float* w;               // fp32 weights [phase][Cout][taps*Cin]
   const unsigned short* w6;     // if set: x6 mode, bf16 split weights [phase][tap][Cin/16][Cout][2][3][8]
   const float* bias;   // may be null
@@ -33,6 +36,8 @@ struct ConvParams {
   float* y;            // v (may be null)
   float* y2;           // silu(v) (may be null)
   float* macc;         // mean accumulator, layout of y (MEAN_* != NONE)
+  unsigned short* y6;  // planes of v (may be null; needs ldy == Cout)
+  unsigned short* y6s; // planes of silu(v) (may be null)
   long long x_bstride;      // elements between clips in x
   long long y_bstride;      // elements between clips in y / y2 / res / macc
   long long w_phase_stride; // elements between phases in w
@@ -54,13 +59,15 @@ int vq_argmin_ntiles(int ncodes);
 hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows, int ntiles, int32_t* codes,
                             hipStream_t s);
 hipError_t launch_row_sqnorm(const float* x, long long rows, int C, float* out, hipStream_t s);
-hipError_t launch_ln_rows(const float* x, float* y, const float* w, const float* b, long long rows, int C, float eps,
-                          int channels_first_form, hipStream_t s);
-hipError_t launch_dwconv_ln(const float* x, float* y, const float* dww, const float* dwb, const float* lnw,
-                            const float* lnb, int batch, int L, int C, hipStream_t s);
-hipError_t launch_frame_pad(const float* audio, float* frames, int batch, long long n, int rows, int hop, int pad_left,
-                            hipStream_t s);
-hipError_t launch_spec_mag(const float* spec, float* mag, long long rows, int nbins, int ld_out, hipStream_t s);
+hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, const float* w, const float* b, long long rows,
+                          int C, float eps, int channels_first_form, hipStream_t s);
+hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, const float* dww, const float* dwb,
+                            const float* lnw, const float* lnb, int batch, int L, int C, hipStream_t s);
+hipError_t launch_frame_pad(const float* audio, float* frames, unsigned short* frames6, int batch, long long n, int rows,
+                            int hop, int pad_left, hipStream_t s);
+hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, long long rows, int nbins, int ld_out,
+                           hipStream_t s);
+hipError_t launch_split_planes(const float* x, unsigned short* y6, long long rows, int C, hipStream_t s);
 hipError_t launch_gather_rows(const float* table, int ntable, const int32_t* idx, long long rows, int width,
                               float* out, int32_t* n_invalid, hipStream_t s);
 hipError_t launch_conv_post_tanh(const float* x, const float* w, float bias, float* out, int batch, int L, int C,

@@ -3,6 +3,7 @@
 // codebook gathers, the VQ partial-argmin reduction, conv_post + tanh, and a batched transpose.
 // All use 16-byte accesses along the contiguous channel axis (channels-last layout).
 #include "dcx_kernels.h"
+#include "dcx_planes.h"
 
 namespace dcx {
 
@@ -22,7 +23,8 @@ __device__ __forceinline__ float wave_sum(float v) {
 // ---------------------------------------------------------------------------------------------
 template <int NV>
 __device__ __forceinline__ void ln_finish(f32x4 (&v)[NV], int C, float eps, int cf, const float* __restrict__ w,
-                                          const float* __restrict__ b, float* __restrict__ yrow, int lane) {
+                                          const float* __restrict__ b, float* __restrict__ yrow,
+                                          unsigned short* __restrict__ y6, long long row, int lane) {
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
@@ -47,14 +49,15 @@ __device__ __forceinline__ void ln_finish(f32x4 (&v)[NV], int C, float eps, int 
     } else {
       o = (v[i] - mean) * rstd * wv + bv;
     }
-    *reinterpret_cast<f32x4*>(yrow + c) = o;
+    if (yrow) *reinterpret_cast<f32x4*>(yrow + c) = o;
+    if (y6) store_planes4(y6, row, C, c, o.x, o.y, o.z, o.w);
   }
 }
 
 template <int NV>
 __global__ void __launch_bounds__(256) ln_rows_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                       const float* __restrict__ w, const float* __restrict__ b,
-                                                       long long rows, float eps, int cf) {
+                                                       unsigned short* __restrict__ y6, const float* __restrict__ w,
+                                                       const float* __restrict__ b, long long rows, float eps, int cf) {
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -62,17 +65,17 @@ __global__ void __launch_bounds__(256) ln_rows_kernel(const float* __restrict__ 
   f32x4 v[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) v[i] = *reinterpret_cast<const f32x4*>(x + row * C + (lane + 64 * i) * 4);
-  ln_finish<NV>(v, C, eps, cf, w, b, y + row * C, lane);
+  ln_finish<NV>(v, C, eps, cf, w, b, y ? y + row * C : nullptr, y6, row, lane);
 }
 
-hipError_t launch_ln_rows(const float* x, float* y, const float* w, const float* b, long long rows, int C, float eps,
-                          int cf, hipStream_t s) {
+hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, const float* w, const float* b, long long rows,
+                          int C, float eps, int cf, hipStream_t s) {
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   switch (C) {
-    case 256: hipLaunchKernelGGL(ln_rows_kernel<1>, grid, block, 0, s, x, y, w, b, rows, eps, cf); break;
-    case 512: hipLaunchKernelGGL(ln_rows_kernel<2>, grid, block, 0, s, x, y, w, b, rows, eps, cf); break;
-    case 768: hipLaunchKernelGGL(ln_rows_kernel<3>, grid, block, 0, s, x, y, w, b, rows, eps, cf); break;
-    case 1024: hipLaunchKernelGGL(ln_rows_kernel<4>, grid, block, 0, s, x, y, w, b, rows, eps, cf); break;
+    case 256: hipLaunchKernelGGL(ln_rows_kernel<1>, grid, block, 0, s, x, y, y6, w, b, rows, eps, cf); break;
+    case 512: hipLaunchKernelGGL(ln_rows_kernel<2>, grid, block, 0, s, x, y, y6, w, b, rows, eps, cf); break;
+    case 768: hipLaunchKernelGGL(ln_rows_kernel<3>, grid, block, 0, s, x, y, y6, w, b, rows, eps, cf); break;
+    case 1024: hipLaunchKernelGGL(ln_rows_kernel<4>, grid, block, 0, s, x, y, y6, w, b, rows, eps, cf); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -82,6 +85,7 @@ hipError_t launch_ln_rows(const float* x, float* y, const float* w, const float*
 // F.layer_norm over channels.  dww is packed [7][C].  One wave per output row.
 template <int NV>
 __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                         unsigned short* __restrict__ y6,
                                                          const float* __restrict__ dww, const float* __restrict__ dwb,
                                                          const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                          int L, long long rows) {
@@ -108,18 +112,18 @@ __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict_
     }
     v[i] = acc + *reinterpret_cast<const f32x4*>(dwb + c);
   }
-  ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y + row * C, lane);
+  ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y ? y + row * C : nullptr, y6, row, lane);
 }
 
-hipError_t launch_dwconv_ln(const float* x, float* y, const float* dww, const float* dwb, const float* lnw,
-                            const float* lnb, int batch, int L, int C, hipStream_t s) {
+hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, const float* dww, const float* dwb,
+                            const float* lnw, const float* lnb, int batch, int L, int C, hipStream_t s) {
   const long long rows = (long long)batch * L;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   switch (C) {
-    case 256: hipLaunchKernelGGL(dwconv_ln_kernel<1>, grid, block, 0, s, x, y, dww, dwb, lnw, lnb, L, rows); break;
-    case 512: hipLaunchKernelGGL(dwconv_ln_kernel<2>, grid, block, 0, s, x, y, dww, dwb, lnw, lnb, L, rows); break;
-    case 768: hipLaunchKernelGGL(dwconv_ln_kernel<3>, grid, block, 0, s, x, y, dww, dwb, lnw, lnb, L, rows); break;
-    case 1024: hipLaunchKernelGGL(dwconv_ln_kernel<4>, grid, block, 0, s, x, y, dww, dwb, lnw, lnb, L, rows); break;
+    case 256: hipLaunchKernelGGL(dwconv_ln_kernel<1>, grid, block, 0, s, x, y, y6, dww, dwb, lnw, lnb, L, rows); break;
+    case 512: hipLaunchKernelGGL(dwconv_ln_kernel<2>, grid, block, 0, s, x, y, y6, dww, dwb, lnw, lnb, L, rows); break;
+    case 768: hipLaunchKernelGGL(dwconv_ln_kernel<3>, grid, block, 0, s, x, y, y6, dww, dwb, lnw, lnb, L, rows); break;
+    case 1024: hipLaunchKernelGGL(dwconv_ln_kernel<4>, grid, block, 0, s, x, y, y6, dww, dwb, lnw, lnb, L, rows); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -129,48 +133,89 @@ hipError_t launch_dwconv_ln(const float* x, float* y, const float* dww, const fl
 // STFT framing: reflect pad ((win-hop)/2 each side, mel_spec.py:30-37) and cut the padded
 // signal into rows of `hop` samples, so frame f = rows f..f+3 (a 4-tap conv over 256 channels).
 // ---------------------------------------------------------------------------------------------
-__global__ void frame_pad_kernel(const float* __restrict__ audio, float* __restrict__ frames, long long n, int rows,
-                                 int hop, int pad_left) {
+__global__ void frame_pad_kernel(const float* __restrict__ audio, float* __restrict__ frames,
+                                 unsigned short* __restrict__ frames6, long long n, int rows, int hop, int pad_left) {
   const int b = blockIdx.y;
-  const long long total = (long long)rows * hop;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    long long src = i - pad_left;
-    if (src < 0) src = -src;
-    if (src >= n) src = 2 * (n - 1) - src;
-    frames[(long long)b * total + i] = audio[(long long)b * n + src];
+  const long long total4 = (long long)rows * hop / 4;
+  for (long long i4 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i4 < total4;
+       i4 += (long long)gridDim.x * blockDim.x) {
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      long long src = i4 * 4 + e - pad_left;
+      if (src < 0) src = -src;
+      if (src >= n) src = 2 * (n - 1) - src;
+      v[e] = audio[(long long)b * n + src];
+    }
+    const long long i = i4 * 4;
+    if (frames) *reinterpret_cast<f32x4*>(frames + (long long)b * rows * hop + i) = f32x4{v[0], v[1], v[2], v[3]};
+    if (frames6) {
+      const long long row = (long long)b * rows + i / hop;
+      store_planes4(frames6, row, hop, (int)(i % hop), v[0], v[1], v[2], v[3]);
+    }
   }
 }
 
-hipError_t launch_frame_pad(const float* audio, float* frames, int batch, long long n, int rows, int hop, int pad_left,
-                            hipStream_t s) {
-  const long long total = (long long)rows * hop;
-  unsigned gx = (unsigned)((total + 255) / 256);
+hipError_t launch_frame_pad(const float* audio, float* frames, unsigned short* frames6, int batch, long long n, int rows,
+                            int hop, int pad_left, hipStream_t s) {
+  if (hop % 8) return hipErrorInvalidValue;
+  const long long total4 = (long long)rows * hop / 4;
+  unsigned gx = (unsigned)((total4 + 255) / 256);
   if (gx > 4096) gx = 4096;
-  hipLaunchKernelGGL(frame_pad_kernel, dim3(gx, batch), dim3(256), 0, s, audio, frames, n, rows, hop, pad_left);
+  hipLaunchKernelGGL(frame_pad_kernel, dim3(gx, batch), dim3(256), 0, s, audio, frames, frames6, n, rows, hop, pad_left);
   return hipGetLastError();
 }
 
 // |STFT| = sqrt(re^2 + im^2 + 1e-6) (mel_spec.py:54-55).  spec columns: [0, nbins) real part of
 // bins 0..nbins-1, [nbins, 2*nbins-2) imaginary part of bins 1..nbins-2 (bins 0 and n_fft/2 are
 // real for a real signal).  Output row padded with zeros to ld_out.
-__global__ void spec_mag_kernel(const float* __restrict__ spec, float* __restrict__ mag, long long rows, int nbins,
-                                int ld_out) {
+__global__ void spec_mag_kernel(const float* __restrict__ spec, float* __restrict__ mag, unsigned short* __restrict__ mag6,
+                                long long rows, int nbins, int ld_out) {
   const long long row = blockIdx.x;
   if (row >= rows) return;
   const int ld_in = 2 * nbins - 2;
-  for (int k = threadIdx.x; k < ld_out; k += blockDim.x) {
-    float o = 0.f;
-    if (k < nbins) {
-      const float re = spec[row * ld_in + k];
-      const float im = (k > 0 && k < nbins - 1) ? spec[row * ld_in + nbins + k - 1] : 0.f;
-      o = sqrtf((re * re + im * im) + 1e-6f);
+  for (int k4 = threadIdx.x * 4; k4 < ld_out; k4 += blockDim.x * 4) {
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = k4 + e;
+      o[e] = 0.f;
+      if (k < nbins) {
+        const float re = spec[row * ld_in + k];
+        const float im = (k > 0 && k < nbins - 1) ? spec[row * ld_in + nbins + k - 1] : 0.f;
+        o[e] = sqrtf((re * re + im * im) + 1e-6f);
+      }
     }
-    mag[row * ld_out + k] = o;
+    if (mag) *reinterpret_cast<f32x4*>(mag + row * ld_out + k4) = f32x4{o[0], o[1], o[2], o[3]};
+    if (mag6) store_planes4(mag6, row, ld_out, k4, o[0], o[1], o[2], o[3]);
   }
 }
 
-hipError_t launch_spec_mag(const float* spec, float* mag, long long rows, int nbins, int ld_out, hipStream_t s) {
-  hipLaunchKernelGGL(spec_mag_kernel, dim3((unsigned)rows), dim3(256), 0, s, spec, mag, rows, nbins, ld_out);
+hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, long long rows, int nbins, int ld_out,
+                           hipStream_t s) {
+  if (ld_out % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(spec_mag_kernel, dim3((unsigned)rows), dim3(256), 0, s, spec, mag, mag6, rows, nbins, ld_out);
+  return hipGetLastError();
+}
+
+// fp32 [rows][C] -> planes (boundary conversion for tensors handed in by the caller).
+__global__ void __launch_bounds__(256) split_planes_kernel(const float* __restrict__ x, unsigned short* __restrict__ y6,
+                                                            long long rows, int C) {
+  const long long total4 = rows * C / 4;
+  for (long long i4 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i4 < total4;
+       i4 += (long long)gridDim.x * blockDim.x) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + i4 * 4);
+    const long long i = i4 * 4;
+    store_planes4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
+  }
+}
+
+hipError_t launch_split_planes(const float* x, unsigned short* y6, long long rows, int C, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  const long long total4 = rows * C / 4;
+  unsigned g = (unsigned)((total4 + 255) / 256);
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(split_planes_kernel, dim3(g), dim3(256), 0, s, x, y6, rows, C);
   return hipGetLastError();
 }
 

@@ -1,0 +1,60 @@
+// Device helpers for the x6 "planes" representation: an fp32 value x is stored as three bf16
+// (hi, mid, lo), round-to-nearest-even each: hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid).
+// Both differences are exact in fp32 and |x - (hi + mid + lo)| <= 2^-27 |x|.  Layout of a planes
+// tensor [rows][C]: per row, per group of 8 channels, 24 bf16 = hi[8] mid[8] lo[8].
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace dcx {
+
+typedef short s16x4p __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned short bf16_bits(float x) {
+  const unsigned u = __float_as_uint(x);
+  return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf16_val(unsigned short b) { return __uint_as_float((unsigned)b << 16); }
+
+__device__ __forceinline__ void split3(float x, unsigned short& h, unsigned short& m, unsigned short& l) {
+  h = bf16_bits(x);
+  const float r1 = x - bf16_val(h);
+  m = bf16_bits(r1);
+  const float r2 = r1 - bf16_val(m);
+  l = bf16_bits(r2);
+}
+
+// Element (row, c) of a planes tensor with C channels: offset of its hi value (mid +8, lo +16).
+__device__ __forceinline__ long long plane_off(long long row, int C, int c) {
+  return row * (long long)C * 3 + (c >> 3) * 24 + (c & 7);
+}
+
+// Store one value (scalar path, e.g. one MFMA accumulator element per lane).
+__device__ __forceinline__ void store_planes1(unsigned short* base, long long row, int C, int c, float v) {
+  unsigned short h, m, l;
+  split3(v, h, m, l);
+  unsigned short* d = base + plane_off(row, C, c);
+  d[0] = h;
+  d[8] = m;
+  d[16] = l;
+}
+
+// Store 4 consecutive channels c..c+3 (c % 4 == 0) of one row: three 8-byte stores.
+__device__ __forceinline__ void store_planes4(unsigned short* base, long long row, int C, int c, float a, float b,
+                                              float cc, float d) {
+  s16x4p hv, mv, lv;
+  const float v[4] = {a, b, cc, d};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    unsigned short h, m, l;
+    split3(v[e], h, m, l);
+    hv[e] = (short)h;
+    mv[e] = (short)m;
+    lv[e] = (short)l;
+  }
+  unsigned short* dst = base + plane_off(row, C, c);
+  *reinterpret_cast<s16x4p*>(dst) = hv;
+  *reinterpret_cast<s16x4p*>(dst + 8) = mv;
+  *reinterpret_cast<s16x4p*>(dst + 16) = lv;
+}
+
+}  // namespace dcx

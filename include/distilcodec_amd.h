@@ -141,7 +141,9 @@ int32_t dcx_get_gemm_mode(const dcx_codec* h);
  * ConvTranspose1d layout [Cin][Cout][k] (transposed=1, padding (k-stride)/2); bias may be NULL.
  * dcx_conv_forward: x [B][Lin][Cin] -> y [B][Lout][Cout] (channels-last, Lout = Lin for a conv
  * with "same" padding, stride*Lin for the transposed form) with epilogue `epi`
- * (0 bias, 1 gelu, 3 residual add: y = res + v), optional second output y_silu = silu(v). */
+ * (0 bias, 1 gelu, 3 residual add: y = res + v), optional second output y_silu = silu(v).
+ * In x6 mode the input is split into planes in a buffer owned by the conv object (allocated on
+ * first use and grown on demand), so unlike the stage calls this test primitive may allocate. */
 typedef struct dcx_conv dcx_conv;
 int dcx_conv_create(const float* weight, const float* bias, int32_t cin, int32_t cout, int32_t k, int32_t dilation,
                     int32_t transposed, int32_t stride, dcx_conv** out);
