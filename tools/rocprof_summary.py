@@ -20,9 +20,15 @@ def short(name):
     if not m:
         return name[:60]
     base, targs = m.group(1), m.group(2) or ""
+    parts = [p.strip() for p in targs.strip("<>").split(",")] if targs else []
     if base == "conv_gemm_f32":
-        parts = [p.strip() for p in targs.strip("<>").split(",")]
-        return f"{'vq_dist_argmin_f32' if parts[-1] == 'true' else 'conv_gemm_f32'}<{parts[0]},{parts[1]}>"
+        kind = "vq_dist_argmin_f32" if parts[-1] == "true" else "conv_gemm_f32"
+        return f"{kind}<{parts[0]},{parts[1]}>"
+    if base == "conv_gemm_x6w8":  # <BM, BN, WM, WN, HALO, ARGMIN>: bench.py's profile names
+        if parts[-1] == "true":
+            return f"vq_dist_argmin_x6w8<{parts[0]},{parts[1]}>"
+        halo = ",halo" if parts[4] != "0" else ""
+        return f"conv_gemm_x6w8<{parts[0]},{parts[1]}{halo}>"
     return base + targs.replace(" ", "")
 
 
