@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--modes", default="x6,f32")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--data", default="randn", choices=["randn", "zero", "bf16"],
+                    help="input values: randn, all zeros, or randn rounded to bf16 (mid/lo planes zero)")
     a = ap.parse_args()
     out = {}
     for name in a.shapes.split(","):
@@ -38,6 +40,10 @@ def main():
         w = (r.standard_normal((cin, cout, k) if tr else (cout, cin, k)) / np.sqrt(cin * k)).astype(np.float32)
         conv = NativeConv(w, np.zeros(cout, np.float32), dilation=d, transposed=tr, stride=s)
         x = torch.randn(B, L, cin, device="cuda")
+        if a.data == "zero":
+            x.zero_()
+        elif a.data == "bf16":
+            x = x.bfloat16().float()
         flops = 2.0 * B * L * (s if tr else 1) * cout * cin * (k // s if tr else k)
         for mode in a.modes.split(","):
             y = conv(x, gemm=mode)
