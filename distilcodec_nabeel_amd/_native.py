@@ -79,6 +79,7 @@ SIGNATURES = {
     "dcx_conv_create": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, ctypes.POINTER(_P)]),
     "dcx_conv_forward": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, _P, _P, _P, _I32, _P]),
     "dcx_conv_destroy": (None, [_P]),
+    "dcx_vq_rescore_stats": (ctypes.c_int, [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I32]),
     "dcx_profile_enable": (ctypes.c_int, [_P, _I32]),
     "dcx_profile_reset": (ctypes.c_int, [_P]),
     "dcx_profile_count": (_I32, [_P]),

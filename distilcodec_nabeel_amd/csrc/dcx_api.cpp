@@ -101,6 +101,8 @@ struct dcx_codec {
   ConvW vq_down, vq_pin, vq_up;
   BlockW vq_down_blk, vq_up_blk;
   float *codebook = nullptr, *e2 = nullptr, *ptable = nullptr;
+  float emax = 0.f, e2max = 0.f;  // largest codebook row norm / squared norm (prefilter bound)
+  int* vq_stats = nullptr;        // [rows rescored, codes rescored] (dcx_vq_rescore_stats)
   unsigned short* codebook6 = nullptr;
   unsigned short* ptable6 = nullptr;  // decode table as activation planes (x6 mode gathers)
   int gemm_mode = DCX_GEMM_X6;
@@ -686,6 +688,7 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   float* x2 = ws.f((size_t)M);
   float* pv = ws.f((size_t)M * ntiles);
   int* pi = ws.i((size_t)M * ntiles);
+  float* pv2 = x6 ? ws.f((size_t)M * ntiles) : nullptr;
   Act zd = conv_input(h, ws, (size_t)M * D);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for vq_encode");
@@ -702,13 +705,23 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
     ConvParams p{};
     p.x = P; p.x6 = P6; p.w = h->codebook; p.w6 = x6 ? h->codebook6 : nullptr;
     p.Cin = CD; p.Cout = NC; p.ldx = CD; p.taps = 1; p.in_step = 1; p.out_mul = 1;
-    p.x2 = x2; p.e2 = h->e2; p.part_val = pv; p.part_idx = pi;
+    p.x2 = x2; p.e2 = h->e2; p.part_val = pv; p.part_idx = pi; p.part_val2 = pv2;
     ProfScope ps(h, s);
     const char* kname = "vq";
-    HIPCHK(h, dcx::launch_vq_argmin(p, (int)M, s, &kname));
-    ps.done(kname, 2.0 * M * NC * CD, 4.0 * ((double)M * CD + (double)NC * CD));
+    if (x6) {
+      HIPCHK(h, dcx::launch_vq_prefilter(p, (int)M, s, &kname));
+      ps.done(kname, 2.0 * M * NC * CD, 4.0 * ((double)M * CD + (double)NC * CD));
+    } else {
+      HIPCHK(h, dcx::launch_vq_argmin(p, (int)M, s, &kname));
+      ps.done(kname, 2.0 * M * NC * CD, 4.0 * ((double)M * CD + (double)NC * CD));
+    }
   }
-  LAUNCH(h, s, "vq_reduce", 0, 8.0 * M * ntiles, dcx::launch_vq_reduce(pv, pi, (int)M, ntiles, codes, s));
+  if (x6)
+    LAUNCH(h, s, "vq_rescore", 0, 12.0 * M * ntiles + 4.0 * M * CD,
+           dcx::launch_vq_rescore(pv, pi, pv2, M, ntiles, NC / ntiles, P, CD, h->codebook, h->emax, h->e2max,
+                                  dcx::kVqPrefilterBound, codes, h->vq_stats, s));
+  else
+    LAUNCH(h, s, "vq_reduce", 0, 8.0 * M * ntiles, dcx::launch_vq_reduce(pv, pi, (int)M, ntiles, codes, s));
   if (fup) LAUNCH(h, s, "gather_rows", 0, 8.0 * M * CD, dcx::launch_gather_rows(h->codebook, NC, codes, M, CD, fup, nullptr, s));
   if (quant) {
     if (x6)
@@ -997,11 +1010,17 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
     auto emb = B.need(q + "grvq.rvqs.0.layers.0._codebook.embed", {1, NC, CD});
     if (emb) {
       std::vector<float> e2(NC);
+      double e2m = 0;
       for (int i = 0; i < NC; ++i) {
         double sacc = 0;
         for (int d = 0; d < CD; ++d) sacc += (double)emb->data[(size_t)i * CD + d] * emb->data[(size_t)i * CD + d];
         e2[i] = (float)sacc;
+        e2m = std::max(e2m, sacc);
       }
+      // rounded up so the prefilter bound stays an upper bound
+      h->e2max = std::nextafter((float)e2m, INFINITY);
+      h->emax = std::nextafter((float)std::sqrt(e2m), INFINITY);
+      h->vq_stats = (int*)B.upload(std::vector<float>(2, 0.f));  // zero counters
       h->codebook = B.upload(emb->data);
       h->codebook6 = B.split_pack(emb->data, 1, NC, 1, CD);
       h->e2 = B.upload(e2);
@@ -1239,6 +1258,18 @@ int dcx_profile_reset(dcx_codec* h) {
     h->prof_launches[i] = 0;
     h->prof_ms[i] = h->prof_flops[i] = h->prof_bytes[i] = 0;
   }
+  return DCX_OK;
+}
+
+int dcx_vq_rescore_stats(dcx_codec* h, int64_t* rows_rescored, int64_t* codes_rescored, int32_t reset) {
+  if (!h || !h->vq_stats) return DCX_ERR_STATE;
+  int v[2] = {0, 0};
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(v, h->vq_stats, sizeof v, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(h, DCX_ERR_HIP, "reading VQ rescore counters failed");
+  if (rows_rescored) *rows_rescored = v[0];
+  if (codes_rescored) *codes_rescored = v[1];
+  if (reset && hipMemset(h->vq_stats, 0, sizeof v) != hipSuccess)
+    return fail(h, DCX_ERR_HIP, "resetting VQ rescore counters failed");
   return DCX_OK;
 }
 

@@ -206,6 +206,74 @@ __device__ __forceinline__ void epilogue(const ConvParams& p, f32x16 (&acc)[BM /
 }
 
 // ---------------------------------------------------------------------------------------------
+// VQ prefilter epilogue: per row of the tile, the smallest and second-smallest approximate
+// squared distance (x2 + e2) - 2 x.e and the code of the smallest (lowest index on ties).
+// vq_rescore_kernel (dcx_misc.hip) certifies the winner or rescores the candidates from these.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void top2_merge(float& v1, int& i1, float& v2, float ov1, int oi1, float ov2) {
+  if (ov1 < v1 || (ov1 == v1 && oi1 < i1)) {
+    v2 = fminf(v1, ov2);
+    v1 = ov1;
+    i1 = oi1;
+  } else {
+    v2 = fminf(v2, ov1);
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void epilogue_top2(const ConvParams& p, f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int q0,
+                                              int co0, int nt, int ntiles, float* smem) {
+  constexpr int WR = BM / WM, WC = BN / WN;
+  constexpr int TM = WR / 32, TN = WC / 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lrow = lane & 31;
+  const int rhalf = 4 * (lane >> 5);
+  __syncthreads();
+  float* rv = smem;                                      // [WN][BM]
+  float* rv2 = smem + WN * BM;                           // [WN][BM]
+  int* ri = reinterpret_cast<int*>(smem + 2 * WN * BM);  // [WN][BM]
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rloc = wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + rhalf;
+      const int q = q0 + rloc;
+      const float xx = (q < p.Lq) ? p.x2[q] : 0.f;
+      float v1 = __builtin_inff(), v2 = __builtin_inff();
+      int i1 = 0x7fffffff;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int co = co0 + wn * WC + j * 32 + lrow;
+        const float d2 = (xx + p.e2[co]) + (-2.0f * acc[i][j][r]);
+        top2_merge(v1, i1, v2, d2, co, __builtin_inff());
+      }
+#pragma unroll
+      for (int off = 16; off >= 1; off >>= 1)
+        top2_merge(v1, i1, v2, __shfl_xor(v1, off, 64), __shfl_xor(i1, off, 64), __shfl_xor(v2, off, 64));
+      if (lrow == 0) {
+        rv[wn * BM + rloc] = v1;
+        rv2[wn * BM + rloc] = v2;
+        ri[wn * BM + rloc] = i1;
+      }
+    }
+  }
+  __syncthreads();
+  for (int rloc = tid; rloc < BM; rloc += blockDim.x) {
+    const int q = q0 + rloc;
+    if (q >= p.Lq) continue;
+    float v1 = rv[rloc], v2 = rv2[rloc];
+    int i1 = ri[rloc];
+#pragma unroll
+    for (int w = 1; w < WN; ++w) top2_merge(v1, i1, v2, rv[w * BM + rloc], ri[w * BM + rloc], rv2[w * BM + rloc]);
+    const long long o = (long long)q * ntiles + nt;
+    p.part_val[o] = v1;
+    p.part_val2[o] = v2;
+    p.part_idx[o] = i1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // fp32 MFMA kernel.  Register-staged double buffer, one barrier per 16-deep K chunk.
 // ---------------------------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, bool ARGMIN>
@@ -331,14 +399,17 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const ConvParams p) {
 // (two register sets, loop unrolled by two), so a step's MFMAs (2 waves x 24 per SIMD = 1536
 // cycles) cover the L2 / Infinity-Cache latency of the tiles two steps out.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN>
+template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN, bool X3 = false>
 __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   static_assert(WM * WN == 8, "8 waves per workgroup");
+  static_assert(!X3 || (ARGMIN && HALO == 0), "the 3-product mode is the VQ prefilter");
+  // X3 (VQ prefilter): only the hi and mid planes are staged and hi*hi + hi*mid + mid*hi issued.
+  constexpr int NPC = X3 ? 4 : 6;  // staged 16-byte pieces per row per K chunk
   constexpr int WR = BM / WM, WC = BN / WN;
   constexpr int TM = WR / 32, TN = WC / 32;
   constexpr int AROWS = BM + HALO;
-  constexpr int A_P = AROWS * 6;  // 16-byte pieces of a staged input tile (planes)
-  constexpr int B_P = BN * 6;
+  constexpr int A_P = AROWS * NPC;  // 16-byte pieces of a staged input tile (planes)
+  constexpr int B_P = BN * NPC;
   constexpr int A_PT = (A_P + 511) / 512, B_PT = (B_P + 511) / 512;
   constexpr int ABUF = AROWS * XROW, BBUF = BN * XROW;
 
@@ -348,8 +419,23 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int ntiles = p.Cout / BN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int mt = wg / ntiles, nt = wg - mt * ntiles;
+  int mt, nt;
+  if constexpr (X3) {
+    // Grouped order: the 256 workgroups resident at once form a 16 (row panels) x 16 (code
+    // tiles) block, each XCD a 4 x 8 sub-block, so every codebook tile is fetched from HBM once
+    // per 16 row panels and each panel once per 16 tiles (ntiles % 16 == 0, launcher-checked).
+    const int mtiles = (p.Lq + BM - 1) / BM;
+    const int bid = blockIdx.x, x = bid & 7, l = (bid >> 3) & 31, sup = bid >> 8;
+    const int nsm = (mtiles + 15) >> 4;
+    const int sm = sup % nsm, sn = sup / nsm;
+    mt = sm * 16 + (x & 3) * 4 + (l & 3);
+    nt = sn * 16 + (x >> 2) * 8 + (l >> 2);
+    if (mt >= mtiles) return;  // whole workgroup, before any barrier
+  } else {
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    mt = wg / ntiles;
+    nt = wg - mt * ntiles;
+  }
   const int q0 = mt * BM, co0 = nt * BN;
   const int b = blockIdx.y, ph = blockIdx.z;
   const unsigned short* __restrict__ xb6 = p.x6 + (long long)b * p.x_bstride * 3;
@@ -369,15 +455,17 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
 #pragma unroll
   for (int i = 0; i < A_PT; ++i) {
     const int idx = min(tid + 512 * i, A_P - 1);
-    a_row[i] = idx / 6;
-    a_k[i] = idx - a_row[i] * 6;
+    a_row[i] = idx / NPC;
+    const int k = idx - a_row[i] * NPC;
+    a_k[i] = X3 ? (k >> 1) * 3 + (k & 1) : k;  // piece = half * 3 + plane
   }
   int b_off[B_PT], b_lds[B_PT];
 #pragma unroll
   for (int i = 0; i < B_PT; ++i) {
     const int idx = min(tid + 512 * i, B_P - 1);
-    const int col = idx / 6, piece = idx - col * 6;
-    b_off[i] = idx * 8;
+    const int col = idx / NPC, k = idx - col * NPC;
+    const int piece = X3 ? (k >> 1) * 3 + (k & 1) : k;
+    b_off[i] = (col * 6 + piece) * 8;
     b_lds[i] = col * XROW + piece * 8;
   }
 
@@ -425,13 +513,13 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
     for (int i = 0; i < TM; ++i) {
       const unsigned short* ap = A + (wm * WR + i * 32 + lrow + off) * XROW + hoff;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const s16x8*>(ap + pl * 8);
+      for (int pl = 0; pl < (X3 ? 2 : 3); ++pl) a[i][pl] = *reinterpret_cast<const s16x8*>(ap + pl * 8);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const unsigned short* bp = Bsm + (wn * WC + j * 32 + lrow) * XROW + hoff;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) bb[j][pl] = *reinterpret_cast<const s16x8*>(bp + pl * 8);
+      for (int pl = 0; pl < (X3 ? 2 : 3); ++pl) bb[j][pl] = *reinterpret_cast<const s16x8*>(bp + pl * 8);
     }
   };
 
@@ -488,9 +576,11 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        DCX_MF(i, j, 2, 0);
-        DCX_MF(i, j, 1, 1);
-        DCX_MF(i, j, 0, 2);
+        if constexpr (!X3) {
+          DCX_MF(i, j, 2, 0);
+          DCX_MF(i, j, 1, 1);
+          DCX_MF(i, j, 0, 2);
+        }
         DCX_MF(i, j, 1, 0);
         DCX_MF(i, j, 0, 1);
         DCX_MF(i, j, 0, 0);
@@ -510,7 +600,9 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
     step(s, std::integral_constant<int, 0>{});
     if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>{});
   }
-  if constexpr (ARGMIN)
+  if constexpr (X3)
+    epilogue_top2<BM, BN, WM, WN>(p, acc, q0, co0, nt, ntiles, reinterpret_cast<float*>(lds));
+  else if constexpr (ARGMIN)
     epilogue<BM, BN, WM, WN, true>(p, acc, q0, co0, nt, ntiles, b, ph, reinterpret_cast<float*>(lds));
   else
     epilogue_lds<BM, BN, WM, WN, (2 * ABUF + 3 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
@@ -576,12 +668,30 @@ hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const 
   ConvParams q = p;
   q.Lq = rows;
   q.Lin = rows;
-  if (p.w6) {
-    if (kname) *kname = "vq_dist_argmin_x6w8<256,128>";
-    return launch_x6w8<256, 128, 4, 2, 0, true>(q, 1, 1, s);
-  }
+  if (p.w6) return hipErrorInvalidValue;  // x6 mode searches with launch_vq_prefilter + rescore
   if (kname) *kname = "vq_dist_argmin_f32<128,128>";
   return launch_f32<128, 128, 2, 2, true>(q, 1, 1, s);
+}
+
+// bf16x3 prefilter of the VQ search (x6 mode).  With x = h + m + l per operand (dcx_planes.h,
+// u = 2^-8), dropping h*l', m*m', l*h' and smaller leaves an error <= 3.1 u^2 sum_k |x_k e_k|
+// (4.7e-5); fp32 accumulation of 672 MFMA partial sums adds <= 2688 * 2^-24 (1.6e-4, allowing 4
+// roundings per MFMA).  By Cauchy-Schwarz sum_k |x_k e_k| <= |x| max|e|, so each approximate
+// squared distance is within 2 * kVqPrefilterBound * |x| max|e| + 8 * 2^-24 (|x|^2 + max|e|^2)
+// of the exact one; vq_rescore_kernel uses that bound.
+hipError_t launch_vq_prefilter(const ConvParams& p, int rows, hipStream_t s, const char** kname) {
+  constexpr int BM = 256, BN = 128;
+  if (!p.w6 || !p.x6 || !p.part_val2 || p.Cin % BK || p.Cout % (BN * 16) || rows < 1) return hipErrorInvalidValue;
+  ConvParams q = p;
+  q.Lq = rows;
+  q.Lin = rows;
+  q.taps = 1;
+  const int mtiles = (rows + BM - 1) / BM, ntiles = p.Cout / BN;
+  const int nsm = (mtiles + 15) / 16;
+  dim3 grid((unsigned)(nsm * (ntiles / 16) * 256));
+  if (kname) *kname = "vq_prefilter_x3w8<256,128>";
+  hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, 4, 2, 0, true, true>), grid, dim3(512), 0, s, q);
+  return hipGetLastError();
 }
 
 }  // namespace dcx

@@ -50,12 +50,21 @@ struct ConvParams {
   const float* e2;      // [Cout] squared norms of the codebook rows
   float* part_val;      // [rows][ntiles]
   int* part_idx;        // [rows][ntiles]
+  float* part_val2;     // [rows][ntiles] second-smallest value (VQ prefilter)
 };
 
 // Launchers (all stream-ordered, no allocation).  Return hipError_t of the launch.
 hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname);
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname);
 int vq_argmin_ntiles(int ncodes);
+// VQ search, x6 mode: bf16x3 prefilter (approximate squared distances, per-tile top 2) ...
+hipError_t launch_vq_prefilter(const ConvParams& p, int rows, hipStream_t s, const char** kname);
+// ... then per row: certify the prefilter's winner with a rigorous error bound, or rescore every
+// candidate inside the bound in fp64.  stats (optional): [0] rows rescored, [1] codes rescored.
+constexpr float kVqPrefilterBound = 2.5e-4f;
+hipError_t launch_vq_rescore(const float* part_val, const int* part_idx, const float* part_val2, long long rows,
+                             int ntiles, int tile_codes, const float* x, int dim, const float* codebook, float emax,
+                             float e2max, float cbound, int32_t* codes, int* stats, hipStream_t s);
 hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows, int ntiles, int32_t* codes,
                             hipStream_t s);
 hipError_t launch_row_sqnorm(const float* x, long long rows, int C, float* out, hipStream_t s);

@@ -273,6 +273,148 @@ hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows
   return hipGetLastError();
 }
 
+// VQ search, second half (x6 mode): one workgroup per row.  From the prefilter's per-tile
+// (smallest, second smallest, code of smallest) approximate squared distances:
+//   best = smallest approximate value; thr = best + 2 * bound (launch_vq_prefilter's bound);
+//   a tile is a candidate if its smallest <= thr, and wholly a candidate if its second <= thr.
+// One candidate code: it is the exact argmin; done.  Otherwise every candidate code is rescored
+// with an fp64 dot product and fp64 norms, smallest exact distance, lowest index on ties (the
+// reference's first-index argmax of -dist).
+constexpr int kMaxVqTiles = 512;
+constexpr int kMaxVqDimVec = 16;  // dim <= 16 * 256
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(256) vq_rescore_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
+                                                         const float* __restrict__ pv2, int ntiles, int tile_codes,
+                                                         const float* __restrict__ x, int dim,
+                                                         const float* __restrict__ code, float emax, float e2max,
+                                                         float cbound, int32_t* __restrict__ codes,
+                                                         int* __restrict__ stats) {
+  const long long row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ float s_v[4];
+  __shared__ int s_i[4], s_n[4];
+  __shared__ double s_d[4];
+  __shared__ int s_c[4];
+  __shared__ unsigned char flag[kMaxVqTiles];
+  const float* v1p = pv + row * ntiles;
+  const float* v2p = pv2 + row * ntiles;
+  const int* i1p = pi + row * ntiles;
+
+  // 1. best approximate value, and |x|^2 in fp64 (x held in registers for the rescore)
+  float bv = __builtin_inff();
+  int bi = 0x7fffffff;
+  for (int t = tid; t < ntiles; t += 256) {
+    const float v = v1p[t];
+    const int i = i1p[t];
+    if (v < bv || (v == bv && i < bi)) { bv = v; bi = i; }
+  }
+  const int nvec = dim >> 8;  // float4 per lane
+  f32x4 xr[kMaxVqDimVec];
+  double xx = 0;
+  const float* xrow = x + row * dim;
+#pragma unroll
+  for (int u = 0; u < kMaxVqDimVec; ++u) {
+    xr[u] = u < nvec ? *reinterpret_cast<const f32x4*>(xrow + u * 256 + lane * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    xx += (double)xr[u][0] * xr[u][0] + (double)xr[u][1] * xr[u][1] + (double)xr[u][2] * xr[u][2] +
+          (double)xr[u][3] * xr[u][3];
+  }
+  xx = wave_sum_f64(xx);  // every wave holds the whole row
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float ov = __shfl_xor(bv, off, 64);
+    const int oi = __shfl_xor(bi, off, 64);
+    if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  }
+  if (lane == 0) { s_v[wave] = bv; s_i[wave] = bi; }
+  __syncthreads();
+  bv = s_v[0];
+  bi = s_i[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w)
+    if (s_v[w] < bv || (s_v[w] == bv && s_i[w] < bi)) { bv = s_v[w]; bi = s_i[w]; }
+
+  // 2. candidates inside the bound
+  const double bound = 2.0 * (double)cbound * sqrt(xx) * (double)emax + 8.0 * 0x1p-24 * (xx + (double)e2max);
+  const double thr = (double)bv + 2.0 * bound * (1.0 + 1e-6);
+  int cnt = 0;
+  for (int t = tid; t < ntiles; t += 256) {
+    const double v1 = v1p[t], v2 = v2p[t];
+    const int f = v1 <= thr ? (v2 <= thr ? 2 : 1) : 0;
+    flag[t] = (unsigned char)f;
+    cnt += f == 2 ? tile_codes : f;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+  if (lane == 0) s_n[wave] = cnt;
+  __syncthreads();
+  cnt = s_n[0] + s_n[1] + s_n[2] + s_n[3];
+  if (cnt <= 1) {  // certified (cnt == 0 only for non-finite input: keep the prefilter's pick)
+    if (tid == 0) codes[row] = bi;
+    return;
+  }
+  if (stats && tid == 0) {
+    atomicAdd(&stats[0], 1);
+    atomicAdd(&stats[1], cnt);
+  }
+
+  // 3. exact rescore of the candidates, one code per wave at a time
+  double best = __builtin_inf();
+  int bc = 0x7fffffff;
+  auto eval = [&](int c) {
+    const float* crow = code + (long long)c * dim;
+    double dot = 0, ee = 0;
+#pragma unroll
+    for (int u = 0; u < kMaxVqDimVec; ++u) {
+      if (u < nvec) {
+        const f32x4 e = *reinterpret_cast<const f32x4*>(crow + u * 256 + lane * 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          dot += (double)xr[u][k] * e[k];
+          ee += (double)e[k] * e[k];
+        }
+      }
+    }
+    dot = wave_sum_f64(dot);
+    ee = wave_sum_f64(ee);
+    const double d = (xx + ee) - 2.0 * dot;
+    if (d < best || (d == best && c < bc)) { best = d; bc = c; }
+  };
+  for (int t = 0; t < ntiles; ++t) {
+    const int f = flag[t];
+    if (f == 1) {
+      if (wave == (t & 3)) eval(i1p[t]);
+    } else if (f == 2) {
+      for (int c = t * tile_codes + wave; c < (t + 1) * tile_codes; c += 4) eval(c);
+    }
+  }
+  if (lane == 0) { s_d[wave] = best; s_c[wave] = bc; }
+  __syncthreads();
+  if (tid == 0) {
+    double d = s_d[0];
+    int c = s_c[0];
+    for (int w = 1; w < 4; ++w)
+      if (s_d[w] < d || (s_d[w] == d && s_c[w] < c)) { d = s_d[w]; c = s_c[w]; }
+    codes[row] = c;
+  }
+}
+
+hipError_t launch_vq_rescore(const float* part_val, const int* part_idx, const float* part_val2, long long rows,
+                             int ntiles, int tile_codes, const float* x, int dim, const float* codebook, float emax,
+                             float e2max, float cbound, int32_t* codes, int* stats, hipStream_t s) {
+  if (ntiles < 1 || ntiles > kMaxVqTiles || dim % 256 || dim > 256 * kMaxVqDimVec || rows < 0)
+    return hipErrorInvalidValue;
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(vq_rescore_kernel, dim3((unsigned)rows), dim3(256), 0, s, part_val, part_idx, part_val2, ntiles,
+                     tile_codes, x, dim, codebook, emax, e2max, cbound, codes, stats);
+  return hipGetLastError();
+}
+
 // out[r] = table[idx[r]] (batched_embedding / einx.get_at).  Negative indices wrap like torch
 // indexing; anything still outside [0, ntable) reads row 0 and is counted.
 __global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restrict__ table, int ntable,

@@ -190,6 +190,13 @@ class NativeCodec:
     def profile(self, on: bool):
         self._check(self.L.dcx_profile_enable(self.h, 1 if on else 0))
 
+    def vq_rescore_stats(self, reset: bool = False) -> tuple[int, int]:
+        """(rows rescored, codes rescored) by the x6 VQ search since the last reset (synchronises)."""
+        import ctypes
+        r, c = ctypes.c_int64(0), ctypes.c_int64(0)
+        self._check(self.L.dcx_vq_rescore_stats(self.h, ctypes.byref(r), ctypes.byref(c), int(reset)))
+        return r.value, c.value
+
     def profile_reset(self):
         self._check(self.L.dcx_profile_reset(self.h))
 

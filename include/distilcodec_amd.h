@@ -151,6 +151,12 @@ int dcx_conv_forward(dcx_conv* c, int32_t gemm_mode, const float* x, int32_t bat
                      float* y_silu, const float* res, int32_t epi, void* stream);
 void dcx_conv_destroy(dcx_conv* c);
 
+/* VQ search diagnostics (x6 mode): the search is a bf16x3 prefilter whose winner is certified
+ * by a rigorous error bound; rows with more than one code inside the bound are rescored in fp64.
+ * Returns the cumulative number of such rows and of codes rescored (synchronises the device);
+ * reset != 0 zeroes the counters.  Replaces nothing in the reference (its search is one cdist). */
+int dcx_vq_rescore_stats(dcx_codec* h, int64_t* rows_rescored, int64_t* codes_rescored, int32_t reset);
+
 /* Optional per-kernel timing: when enabled, every launch is bracketed by HIP events on its
  * stream.  dcx_profile_read synchronises the device and returns, per kernel symbol, the
  * launch count, summed device milliseconds and summed algorithmic FLOPs / bytes. */

@@ -1,0 +1,105 @@
+"""GPU VQ search in x6 mode against an exact fp64 argmin.
+
+x6 mode searches with a bf16x3 prefilter and then an fp64 rescore (launch_vq_prefilter /
+vq_rescore_kernel). The prefilter's winner is accepted only when no other code can be inside
+its rigorous error bound. Every other row is rescored in fp64. The search must therefore return
+the exact nearest code for every row, with the lowest index on exact ties (the reference's
+first-index argmax of -dist, vector_quantize_pytorch.py:41-45, :96).
+
+The check runs on our own x_pjt_in, so no tolerance is involved. The fp64 argmin is computed
+with torch on the GPU. It differs from the rescore only in summation order, which cannot move an
+argmin unless two distances agree to about 1e-13.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+KEY = "grvq.rvqs.0.layers.0._codebook.embed"
+
+
+def _argmin_fp64(P: torch.Tensor, E: torch.Tensor, chunk: int = 1024) -> np.ndarray:
+    E64 = E.to("cuda:0", torch.float64)
+    e2 = (E64 ** 2).sum(1)
+    out = []
+    for s in range(0, P.shape[0], chunk):
+        x = P[s: s + chunk].to("cuda:0", torch.float64)
+        d = (x ** 2).sum(1)[:, None] + e2[None, :] - 2.0 * (x @ E64.T)
+        out.append(torch.argmin(d, dim=1).cpu())  # first index of the minimum
+    return torch.cat(out).numpy()
+
+
+@pytest.fixture(scope="module")
+def veng(cfg, state):
+    from distilcodec_nabeel_amd.engine import NativeCodec
+
+    return NativeCodec(cfg, state, "cuda:0", with_generator=False, gemm="x6")
+
+
+def _search(eng, feat):
+    codes, pin, _, _ = eng.vq_encode(feat, want_fup=False, want_quantized=False)
+    return codes.cpu().numpy().reshape(-1), pin.reshape(-1, pin.shape[-1])
+
+
+@pytest.mark.parametrize("name", ["e2e_batch", "e2e_3s", "e2e_real"])
+def test_search_exact_on_fixture_audio(veng, golden, state, name):
+    g = golden[name]
+    feat = veng.encode(torch.from_numpy(g["mel"]).transpose(1, 2))
+    codes, pin = _search(veng, feat)
+    from oracle import reference_cpu as R
+
+    E = R.codebook(state["quantizer"])
+    assert np.array_equal(codes, _argmin_fp64(pin, E))
+
+
+def test_search_exact_many_rows(veng, state):
+    # 4 x 1200 frames: 19 row panels, so the grouped tile order has a partial 16-panel group.
+    g = torch.Generator().manual_seed(5)
+    feat = torch.randn(4, 1200, 1024, generator=g) * 0.5
+    veng.vq_rescore_stats(reset=True)
+    codes, pin = _search(veng, feat)
+    from oracle import reference_cpu as R
+
+    E = R.codebook(state["quantizer"])
+    assert np.array_equal(codes, _argmin_fp64(pin, E))
+    rows, n = veng.vq_rescore_stats()
+    assert 0 <= rows <= codes.size and n >= 2 * rows
+
+
+def test_search_duplicate_codes_lowest_index(cfg, state):
+    """Exact ties: copies of each row's chosen code at other indices, in the same 128-code tile
+    (which forces the whole-tile rescore) and in another tile. The lowest index must win."""
+    from distilcodec_nabeel_amd.engine import NativeCodec
+    from oracle import reference_cpu as R
+
+    g = torch.Generator().manual_seed(11)
+    feat = torch.randn(1, 64, 1024, generator=g) * 0.5
+    base = NativeCodec(cfg, state, "cuda:0", with_generator=False, gemm="x6")
+    codes0, _ = _search(base, feat)
+    del base
+    E = R.codebook(state["quantizer"]).clone()
+    NC = E.shape[0]
+    chosen = sorted(set(codes0.tolist()))[:8]
+    expect = {}
+    for c in chosen:
+        same_tile = c ^ 1
+        other_tile = (c + 4096 + 64) % NC
+        if same_tile in chosen or other_tile in chosen:
+            continue
+        E[same_tile] = E[c]
+        E[other_tile] = E[c]
+        expect[c] = min(c, same_tile, other_tile)
+    assert expect
+    st = {k: dict(v) for k, v in state.items()}
+    st["quantizer"][KEY] = E[None].numpy() if isinstance(state["quantizer"][KEY], np.ndarray) else E[None]
+    eng = NativeCodec(cfg, st, "cuda:0", with_generator=False, gemm="x6")
+    eng.vq_rescore_stats(reset=True)
+    codes, pin = _search(eng, feat)
+    assert np.array_equal(codes, _argmin_fp64(pin, E))
+    hit = [i for i, c in enumerate(codes0) if int(c) in expect]
+    assert hit
+    for i in hit:
+        assert codes[i] == expect[int(codes0[i])]
+    rows, n = eng.vq_rescore_stats()
+    assert rows >= len(hit) and n >= 128 * len(hit)
