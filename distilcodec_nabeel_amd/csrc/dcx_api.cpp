@@ -971,7 +971,7 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
     h->dft.cin = c.hop; h->dft.cout = N; h->dft.taps = N / c.hop; h->dft.in_step = 1;
     h->dft.w = B.upload(basis);
     h->dft.w6 = B.split_pack(basis, 1, N, N / c.hop, c.hop);
-    const int kpad = (nb + 15) / 16 * 16;
+    const int kpad = (nb + 31) / 32 * 32;  // even number of 16-deep chunks (x6 kernels step in pairs)
     std::vector<double> fb = mel_fb(nb, c.f_min, c.f_max, c.n_mels, c.sample_rate);
     std::vector<float> pk((size_t)c.n_mels * kpad, 0.f);
     for (int m = 0; m < c.n_mels; ++m)

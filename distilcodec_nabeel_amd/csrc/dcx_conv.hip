@@ -399,12 +399,10 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const ConvParams p) {
 // (two register sets, loop unrolled by two), so a step's MFMAs (2 waves x 24 per SIMD = 1536
 // cycles) cover the L2 / Infinity-Cache latency of the tiles two steps out.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN, bool X3 = false>
+template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN>
 __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   static_assert(WM * WN == 8, "8 waves per workgroup");
-  static_assert(!X3 || (ARGMIN && HALO == 0), "the 3-product mode is the VQ prefilter");
-  // X3 (VQ prefilter): only the hi and mid planes are staged and hi*hi + hi*mid + mid*hi issued.
-  constexpr int NPC = X3 ? 4 : 6;  // staged 16-byte pieces per row per K chunk
+  constexpr int NPC = 6;  // staged 16-byte pieces per row per K chunk
   constexpr int WR = BM / WM, WC = BN / WN;
   constexpr int TM = WR / 32, TN = WC / 32;
   constexpr int AROWS = BM + HALO;
@@ -419,23 +417,8 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int ntiles = p.Cout / BN;
-  int mt, nt;
-  if constexpr (X3) {
-    // Grouped order: the 256 workgroups resident at once form a 16 (row panels) x 16 (code
-    // tiles) block, each XCD a 4 x 8 sub-block, so every codebook tile is fetched from HBM once
-    // per 16 row panels and each panel once per 16 tiles (ntiles % 16 == 0, launcher-checked).
-    const int mtiles = (p.Lq + BM - 1) / BM;
-    const int bid = blockIdx.x, x = bid & 7, l = (bid >> 3) & 31, sup = bid >> 8;
-    const int nsm = (mtiles + 15) >> 4;
-    const int sm = sup % nsm, sn = sup / nsm;
-    mt = sm * 16 + (x & 3) * 4 + (l & 3);
-    nt = sn * 16 + (x >> 2) * 8 + (l >> 2);
-    if (mt >= mtiles) return;  // whole workgroup, before any barrier
-  } else {
-    const int wg = xcd_remap(blockIdx.x, gridDim.x);
-    mt = wg / ntiles;
-    nt = wg - mt * ntiles;
-  }
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
   const int b = blockIdx.y, ph = blockIdx.z;
   const unsigned short* __restrict__ xb6 = p.x6 + (long long)b * p.x_bstride * 3;
@@ -456,16 +439,14 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   for (int i = 0; i < A_PT; ++i) {
     const int idx = min(tid + 512 * i, A_P - 1);
     a_row[i] = idx / NPC;
-    const int k = idx - a_row[i] * NPC;
-    a_k[i] = X3 ? (k >> 1) * 3 + (k & 1) : k;  // piece = half * 3 + plane
+    a_k[i] = idx - a_row[i] * NPC;  // piece = half * 3 + plane
   }
   int b_off[B_PT], b_lds[B_PT];
 #pragma unroll
   for (int i = 0; i < B_PT; ++i) {
     const int idx = min(tid + 512 * i, B_P - 1);
-    const int col = idx / NPC, k = idx - col * NPC;
-    const int piece = X3 ? (k >> 1) * 3 + (k & 1) : k;
-    b_off[i] = (col * 6 + piece) * 8;
+    const int col = idx / NPC, piece = idx - col * NPC;
+    b_off[i] = idx * 8;
     b_lds[i] = col * XROW + piece * 8;
   }
 
@@ -513,13 +494,13 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
     for (int i = 0; i < TM; ++i) {
       const unsigned short* ap = A + (wm * WR + i * 32 + lrow + off) * XROW + hoff;
 #pragma unroll
-      for (int pl = 0; pl < (X3 ? 2 : 3); ++pl) a[i][pl] = *reinterpret_cast<const s16x8*>(ap + pl * 8);
+      for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const s16x8*>(ap + pl * 8);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const unsigned short* bp = Bsm + (wn * WC + j * 32 + lrow) * XROW + hoff;
 #pragma unroll
-      for (int pl = 0; pl < (X3 ? 2 : 3); ++pl) bb[j][pl] = *reinterpret_cast<const s16x8*>(bp + pl * 8);
+      for (int pl = 0; pl < 3; ++pl) bb[j][pl] = *reinterpret_cast<const s16x8*>(bp + pl * 8);
     }
   };
 
@@ -553,9 +534,14 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   adv(c2, m2);
   int c3 = c2, m3 = m2;  // position of step s+3
   adv(c3, m3);
-  // in flight for the first loop step: B(2) and the input chunk first used at step 2
+  // in flight for the first loop step: the input chunk staged next (1-tap: the one first used at
+  // step 2; with a halo: chunk 1, held in registers until step taps - 2 stores it) and B(2)
+  if constexpr (HALO > 0) {
+    if (nchunks > 1) loadA(1, ra[0]);
+  } else {
+    if (m2 == 0 && c2 < nchunks) loadA(c2, ra[1 % RA_SETS]);
+  }
   loadB(min(c2, nchunks - 1), c2 < nchunks ? m2 : taps - 1, rb[1]);
-  if (m2 == 0 && c2 < nchunks) loadA(c2, ra[1 % RA_SETS]);
   __syncthreads();
   readF(0, 0, 0, af[0], bfr[0]);
 
@@ -563,11 +549,19 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   auto step = [&](int s, auto qtag) {
     constexpr int Q = decltype(qtag)::value;
     const int slot1 = slot == 2 ? 0 : slot + 1, slot2 = slot1 == 2 ? 0 : slot1 + 1;
-    // 1. fragments of step s+1 (its data was made visible by the previous barrier)
-    if (s + 1 < nsteps) readF(c1, m1, slot1, af[1 - Q], bfr[1 - Q]);
-    // 2. global loads for step s+3 (B) and for the input chunk first used at step s+3
+    // 1. fragments of step s+1 (its data was made visible by the previous barrier; after the
+    //    last step this reads unused LDS, which keeps the step free of branches)
+    readF(c1, m1, slot1, af[1 - Q], bfr[1 - Q]);
+    // 2. global loads: the input chunk first (so the compiler's merged wait for a chunk store never
+    //    covers this step's weight loads), then B for step s+3.  1-tap: the chunk first used at
+    //    step s+3.  With a halo: chunk c1 + 1 on the last step of a chunk, taps - 1 steps before
+    //    step (c1, taps - 2) stores it (one register set: the previous chunk is stored by then).
+    if constexpr (HALO > 0) {
+      if (m1 == 0 && c1 + 1 < nchunks) loadA(c1 + 1, ra[0]);
+    } else {
+      if (m3 == 0 && c3 < nchunks) loadA(c3, ra[Q % RA_SETS]);
+    }
     loadB(min(c3, nchunks - 1), c3 < nchunks ? m3 : taps - 1, rb[Q]);
-    if (m3 == 0 && c3 < nchunks) loadA(c3, ra[Q % RA_SETS]);
     // 3. MFMAs of step s
 #define DCX_MF(i, j, x, y) \
   acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[Q][i][x]), \
@@ -576,11 +570,9 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        if constexpr (!X3) {
-          DCX_MF(i, j, 2, 0);
-          DCX_MF(i, j, 1, 1);
-          DCX_MF(i, j, 0, 2);
-        }
+        DCX_MF(i, j, 2, 0);
+        DCX_MF(i, j, 1, 1);
+        DCX_MF(i, j, 0, 2);
         DCX_MF(i, j, 1, 0);
         DCX_MF(i, j, 0, 1);
         DCX_MF(i, j, 0, 0);
@@ -596,16 +588,179 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
     slot = slot1;
     (void)c;
   };
+  // nsteps is even (launcher): without an odd exit the loop header never merges a path on which
+  // this iteration's loads are still in flight, which made the waitcnt pass emit vmcnt(0).
   for (int s = 0; s < nsteps; s += 2) {
     step(s, std::integral_constant<int, 0>{});
-    if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>{});
+    step(s + 1, std::integral_constant<int, 1>{});
   }
-  if constexpr (X3)
-    epilogue_top2<BM, BN, WM, WN>(p, acc, q0, co0, nt, ntiles, reinterpret_cast<float*>(lds));
-  else if constexpr (ARGMIN)
+  if constexpr (ARGMIN)
     epilogue<BM, BN, WM, WN, true>(p, acc, q0, co0, nt, ntiles, b, ph, reinterpret_cast<float*>(lds));
   else
     epilogue_lds<BM, BN, WM, WN, (2 * ABUF + 3 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+}
+
+// ---------------------------------------------------------------------------------------------
+// VQ prefilter GEMM (x6 mode): approximate x.e from hi*hi + hi*mid + mid*hi of the planes
+// (bound in launch_vq_prefilter), per-tile top 2 of (x2 + e2) - 2 x.e (epilogue_top2).
+//
+// Same 8-wave / 256x128 / 64x64-per-wave shape as conv_gemm_x6w8, but a step covers K = 32 (two
+// 16-deep sub-chunks, hi and mid planes only: 8 pieces of 16 B per row in a 144-byte LDS row,
+// 36 dwords, conflict-free for b128 reads), so a step is 2 x 12 MFMAs per wave like the convs'.
+// Fragments are single-buffered per sub-chunk: sub-chunk 0 of step s+1 is read from LDS while
+// sub-chunk 1 of step s is on the matrix cores, and vice versa.  Loads run three steps ahead
+// (input tile double buffer, weight ring of 3), stores two.
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(512) vq_prefilter_x3(const ConvParams p) {
+  static_assert(WM * WN == 8, "8 waves per workgroup");
+  constexpr int WR = BM / WM, WC = BN / WN;
+  constexpr int TM = WR / 32, TN = WC / 32;
+  constexpr int ROW = 72;  // ushort per LDS row: 8 pieces + 1 pad piece
+  constexpr int A_PT = BM * 8 / 512, B_PT = BN * 8 / 512;
+  static_assert(BM * 8 % 512 == 0 && BN * 8 % 512 == 0, "staging pieces per thread");
+  constexpr int ABUF = BM * ROW, BBUF = BN * ROW;
+  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * ABUF + 3 * BBUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int ntiles = p.Cout / BN;
+  // grouped order: 16 row panels x 16 code tiles resident together, 4 x 8 per XCD (ntiles % 16 == 0)
+  const int mtiles = (p.Lq + BM - 1) / BM;
+  const int bid = blockIdx.x, xc = bid & 7, l = (bid >> 3) & 31, sup = bid >> 8;
+  const int nsm = (mtiles + 15) >> 4;
+  const int mt = (sup % nsm) * 16 + (xc & 3) * 4 + (l & 3);
+  const int nt = (sup / nsm) * 16 + (xc >> 2) * 8 + (l >> 2);
+  if (mt >= mtiles) return;  // whole workgroup, before any barrier
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int nsteps = p.Cin / 32;
+  const long long ldx6 = (long long)p.ldx * 3;
+  const long long wslab = (long long)p.Cout * 48;  // one 16-deep chunk of the split codebook
+
+  // staging slots: piece k of a row = (sub u = k >> 2, half h = (k >> 1) & 1, plane k & 1)
+  const unsigned short* a_src[A_PT];
+  int a_lds[A_PT];
+#pragma unroll
+  for (int i = 0; i < A_PT; ++i) {
+    const int idx = tid + 512 * i, row = idx >> 3, k = idx & 7;
+    const int q = q0 + row;
+    const int goff = (k >> 2) * 48 + ((k >> 1) & 1) * 24 + (k & 1) * 8;
+    a_src[i] = q < p.Lq ? p.x6 + (long long)q * ldx6 + goff : reinterpret_cast<const unsigned short*>(g_zero_row);
+    a_lds[i] = row * ROW + k * 8;
+  }
+  const int a_step = 96;  // ushort per step along a row (zero-page rows must not advance)
+  bool a_live[A_PT];
+#pragma unroll
+  for (int i = 0; i < A_PT; ++i) a_live[i] = q0 + ((tid + 512 * i) >> 3) < p.Lq;
+  long long b_off[B_PT];
+  int b_lds[B_PT];
+#pragma unroll
+  for (int i = 0; i < B_PT; ++i) {
+    const int idx = tid + 512 * i, col = idx >> 3, k = idx & 7;
+    b_off[i] = (long long)(co0 + col) * 48 + (k >> 2) * wslab + ((k >> 1) & 1) * 24 + (k & 1) * 8;
+    b_lds[i] = col * ROW + k * 8;
+  }
+
+  f32x4 ra[2][A_PT], rb[2][B_PT];
+  auto loadA = [&](int s, f32x4(&r)[A_PT]) {
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i)
+      r[i] = *reinterpret_cast<const f32x4*>(a_src[i] + (a_live[i] ? s * a_step : 0));
+  };
+  auto loadB = [&](int s, f32x4(&r)[B_PT]) {
+    const unsigned short* base = p.w6 + (long long)s * 2 * wslab;
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) r[i] = *reinterpret_cast<const f32x4*>(base + b_off[i]);
+  };
+  auto storeA = [&](int buf, const f32x4(&r)[A_PT]) {
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) *reinterpret_cast<f32x4*>(lds + buf * ABUF + a_lds[i]) = r[i];
+  };
+  auto storeB = [&](int slot, const f32x4(&r)[B_PT]) {
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) *reinterpret_cast<f32x4*>(lds + 2 * ABUF + slot * BBUF + b_lds[i]) = r[i];
+  };
+
+  const int lrow = lane & 31;
+  const int hoff = (lane >> 5) * 16;  // K half: pieces (h, hi), (h, mid)
+  s16x8 fa[2][TM][2], fb[2][TN][2];   // [sub][tile][plane]
+  auto readSub = [&](int buf, int slot, int u) {
+    const unsigned short* A = lds + buf * ABUF + u * 32 + hoff;
+    const unsigned short* Bs = lds + 2 * ABUF + slot * BBUF + u * 32 + hoff;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const unsigned short* ap = A + (wm * WR + i * 32 + lrow) * ROW;
+      fa[u][i][0] = *reinterpret_cast<const s16x8*>(ap);
+      fa[u][i][1] = *reinterpret_cast<const s16x8*>(ap + 8);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const unsigned short* bp = Bs + (wn * WC + j * 32 + lrow) * ROW;
+      fb[u][j][0] = *reinterpret_cast<const s16x8*>(bp);
+      fb[u][j][1] = *reinterpret_cast<const s16x8*>(bp + 8);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  auto mfmaSub = [&](int u) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[u][i][1]),
+                                                            __builtin_bit_cast(bf16x8, fb[u][j][0]), acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[u][i][0]),
+                                                            __builtin_bit_cast(bf16x8, fb[u][j][1]), acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[u][i][0]),
+                                                            __builtin_bit_cast(bf16x8, fb[u][j][0]), acc[i][j], 0, 0, 0);
+      }
+  };
+
+  // prologue: steps 0 and 1 staged, step 2 in flight
+  loadA(0, ra[0]);
+  loadB(0, rb[0]);
+  storeA(0, ra[0]);
+  storeB(0, rb[0]);
+  const int s1 = min(1, nsteps - 1), s2 = min(2, nsteps - 1);
+  loadA(s1, ra[0]);
+  loadB(s1, rb[0]);
+  storeA(1, ra[0]);
+  storeB(1, rb[0]);
+  loadA(s2, ra[1]);
+  loadB(s2, rb[1]);
+  __syncthreads();
+  readSub(0, 0, 0);
+  readSub(0, 0, 1);
+
+  int slot = 0;
+  auto step = [&](int s, auto qtag) {
+    constexpr int Q = decltype(qtag)::value;
+    const int slot1 = slot == 2 ? 0 : slot + 1, slot2 = slot1 == 2 ? 0 : slot1 + 1;
+    const int s3 = min(s + 3, nsteps - 1);
+    loadA(s3, ra[Q]);
+    loadB(s3, rb[Q]);
+    mfmaSub(0);
+    readSub((s + 1) & 1, slot1, 0);  // after the last step: reads unused data, no branch
+    mfmaSub(1);
+    readSub((s + 1) & 1, slot1, 1);
+    storeB(slot2, rb[1 - Q]);
+    storeA(s & 1, ra[1 - Q]);  // step s+2's tile into the buffer step s used
+    __syncthreads();
+    slot = slot1;
+  };
+  // nsteps is even (launcher): no odd exit, so the loop header never merges a path with this
+  // step's loads still in flight (which made the waitcnt pass drain everything, vmcnt(0))
+  for (int s = 0; s < nsteps; s += 2) {
+    step(s, std::integral_constant<int, 0>{});
+    step(s + 1, std::integral_constant<int, 1>{});
+  }
+  epilogue_top2<BM, BN, WM, WN>(p, acc, q0, co0, nt, ntiles, reinterpret_cast<float*>(lds));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -633,7 +788,7 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
   if (p.Cin % BK || p.Cout % 32 || phases < 1 || phases > kMaxPhases) return hipErrorInvalidValue;
   if (p.w6) {
     const int span = tap_span(p);
-    if (span > 64) return hipErrorInvalidValue;
+    if (span > 64 || (p.Cin / BK) * p.taps % 2) return hipErrorInvalidValue;
     const bool h = span > 0;
     if (p.Cout % 128 == 0) {
       if (kname) *kname = h ? "conv_gemm_x6w8<256,128,halo>" : "conv_gemm_x6w8<256,128>";
@@ -689,8 +844,9 @@ hipError_t launch_vq_prefilter(const ConvParams& p, int rows, hipStream_t s, con
   const int mtiles = (rows + BM - 1) / BM, ntiles = p.Cout / BN;
   const int nsm = (mtiles + 15) / 16;
   dim3 grid((unsigned)(nsm * (ntiles / 16) * 256));
-  if (kname) *kname = "vq_prefilter_x3w8<256,128>";
-  hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, 4, 2, 0, true, true>), grid, dim3(512), 0, s, q);
+  if (p.Cin % 64) return hipErrorInvalidValue;  // even number of K32 steps
+  if (kname) *kname = "vq_prefilter_x3<256,128>";
+  hipLaunchKernelGGL((vq_prefilter_x3<BM, BN, 4, 2>), grid, dim3(512), 0, s, q);
   return hipGetLastError();
 }
 

@@ -24,6 +24,8 @@ def short(name):
     if base == "conv_gemm_f32":
         kind = "vq_dist_argmin_f32" if parts[-1] == "true" else "conv_gemm_f32"
         return f"{kind}<{parts[0]},{parts[1]}>"
+    if base == "vq_prefilter_x3":
+        return f"vq_prefilter_x3<{parts[0]},{parts[1]}>"
     if base == "conv_gemm_x6w8":  # <BM, BN, WM, WN, HALO, ARGMIN, X3>: bench.py's profile names
         if len(parts) > 6 and parts[6] == "true":
             return f"vq_prefilter_x3w8<{parts[0]},{parts[1]}>"
