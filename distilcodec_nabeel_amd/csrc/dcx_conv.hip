@@ -39,7 +39,22 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int BK = 16;    // K chunk per pipeline stage (both modes)
 constexpr int LDSK = 20;  // f32 mode: padded LDS row (floats); 20*i mod 64 distinct per b128 group
-constexpr int XROW = 56;  // x6 mode: LDS row = [half 2][plane 3][8] bf16 + 8 pad (112 B; 28*i mod 64 distinct)
+// x6 mode LDS rows hold [half 2][plane 3][8] bf16 = 96 B of one row / column.  Two layouts, both
+// conflict-free for ds_read_b128 of one piece by 16 lanes on 16 consecutive rows (any tap offset):
+//  * padded (8-wave kernels): 112-byte rows, 28 r mod 64 distinct;
+//  * swizzled (4-wave kernels, which must stay under 80 KB for two workgroups per CU): 96-byte
+//    rows, and rows with bit 3 set store their two K halves swapped, so rows r and r+8 differ in
+//    the parity of their 16-byte bank group (6 r + piece mod 16).  Measured 1-2 % slower than the
+//    padded rows on the 8-wave kernels (the per-row XOR), hence only where LDS requires it.
+template <bool SWZ>
+struct XRow {
+  static constexpr int kStride = SWZ ? 48 : 56;  // ushort
+  __device__ static __forceinline__ int half(int row, int h) { return SWZ ? h ^ ((row >> 3) & 1) : h; }
+  __device__ static __forceinline__ int off(int row, int piece) {  // piece = half * 3 + plane
+    const int h = piece >= 3;
+    return row * kStride + (half(row, h) * 3 + piece - 3 * h) * 8;
+  }
+};
 
 __device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
 __device__ __forceinline__ float gelu_f(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f)); }
@@ -394,21 +409,25 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const ConvParams p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// x6, 8-wave variant (512 threads, 2 waves per SIMD), block tile 256 x 128, wave tile 64 x 64.
+// x6 kernel, WM x WN = 8 waves (512 threads) or 4 waves (256 threads, two workgroups per CU for
+// the small-Cout tiles); 2 waves per SIMD either way.  Block tile 256 x 128 has wave tile 64 x 64.
 // Same arithmetic and LDS images as conv_gemm_x6; the loads run two K16 steps ahead of their use
 // (two register sets, loop unrolled by two), so a step's MFMAs (2 waves x 24 per SIMD = 1536
 // cycles) cover the L2 / Infinity-Cache latency of the tiles two steps out.
 // ---------------------------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN>
-__global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
-  static_assert(WM * WN == 8, "8 waves per workgroup");
+__global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams p) {
+  static_assert(WM * WN == 8 || WM * WN == 4, "4 or 8 waves per workgroup");
+  constexpr int NT = 64 * WM * WN;
+  using XR = XRow<WM * WN == 4>;
+  constexpr int XROW = XR::kStride;
   constexpr int NPC = 6;  // staged 16-byte pieces per row per K chunk
   constexpr int WR = BM / WM, WC = BN / WN;
   constexpr int TM = WR / 32, TN = WC / 32;
   constexpr int AROWS = BM + HALO;
   constexpr int A_P = AROWS * NPC;  // 16-byte pieces of a staged input tile (planes)
   constexpr int B_P = BN * NPC;
-  constexpr int A_PT = (A_P + 511) / 512, B_PT = (B_P + 511) / 512;
+  constexpr int A_PT = (A_P + NT - 1) / NT, B_PT = (B_P + NT - 1) / NT;
   constexpr int ABUF = AROWS * XROW, BBUF = BN * XROW;
 
   // LDS: input tiles (2, by chunk parity) + weight-tile ring (3, by step mod 3).
@@ -434,20 +453,21 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   const int lin = p.Lin;
 
   // Branch-free staging slots (surplus slots duplicate the last element).
-  int a_row[A_PT], a_k[A_PT];
+  int a_row[A_PT], a_k[A_PT], a_lds[A_PT];
 #pragma unroll
   for (int i = 0; i < A_PT; ++i) {
-    const int idx = min(tid + 512 * i, A_P - 1);
+    const int idx = min(tid + NT * i, A_P - 1);
     a_row[i] = idx / NPC;
     a_k[i] = idx - a_row[i] * NPC;  // piece = half * 3 + plane
+    a_lds[i] = XR::off(a_row[i], a_k[i]);
   }
   int b_off[B_PT], b_lds[B_PT];
 #pragma unroll
   for (int i = 0; i < B_PT; ++i) {
-    const int idx = min(tid + 512 * i, B_P - 1);
+    const int idx = min(tid + NT * i, B_P - 1);
     const int col = idx / NPC, piece = idx - col * NPC;
     b_off[i] = idx * 8;
-    b_lds[i] = col * XROW + piece * 8;
+    b_lds[i] = XR::off(col, piece);
   }
 
   // With a tap halo (taps >= 2) at most one input-chunk load is in flight, so one register set
@@ -469,7 +489,7 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   auto storeA = [&](int buf, const f32x4(&r)[A_PT]) {
     unsigned short* A = lds + buf * ABUF;
 #pragma unroll
-    for (int i = 0; i < A_PT; ++i) *reinterpret_cast<f32x4*>(A + a_row[i] * XROW + a_k[i] * 8) = r[i];
+    for (int i = 0; i < A_PT; ++i) *reinterpret_cast<f32x4*>(A + a_lds[i]) = r[i];
   };
   auto loadB = [&](int c, int m, f32x4(&r)[B_PT]) {
     const unsigned short* src = wbase + ((long long)m * nchunks + c) * wslab;
@@ -483,7 +503,13 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   };
 
   const int lrow = lane & 31;
-  const int hoff = (lane >> 5) * 24;
+  const int khalf = lane >> 5;
+  int b_frag[TN];  // LDS offsets of this lane's weight-fragment rows (bit 3 is fixed per lane)
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cc = wn * WC + j * 32 + lrow;
+    b_frag[j] = cc * XROW + XR::half(cc, khalf) * 24;
+  }
   s16x8 af[2][TM][3], bfr[2][TN][3];
   // fragments of step (c, m) in ring slot `slot` -> register set F
   auto readF = [&](int c, int m, int slot, s16x8(&a)[TM][3], s16x8(&bb)[TN][3]) {
@@ -492,13 +518,14 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
     const unsigned short* Bsm = lds + 2 * ABUF + slot * BBUF;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const unsigned short* ap = A + (wm * WR + i * 32 + lrow + off) * XROW + hoff;
+      const int rr = wm * WR + i * 32 + lrow + off;
+      const unsigned short* ap = A + rr * XROW + XR::half(rr, khalf) * 24;
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const s16x8*>(ap + pl * 8);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const unsigned short* bp = Bsm + (wn * WC + j * 32 + lrow) * XROW + hoff;
+      const unsigned short* bp = Bsm + b_frag[j];
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) bb[j][pl] = *reinterpret_cast<const s16x8*>(bp + pl * 8);
     }
@@ -597,7 +624,7 @@ __global__ void __launch_bounds__(512) conv_gemm_x6w8(const ConvParams p) {
   if constexpr (ARGMIN)
     epilogue<BM, BN, WM, WN, true>(p, acc, q0, co0, nt, ntiles, b, ph, reinterpret_cast<float*>(lds));
   else
-    epilogue_lds<BM, BN, WM, WN, (2 * ABUF + 3 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+    epilogue_lds<BM, BN, WM, WN, (2 * ABUF + 3 * BBUF) / 2, NT>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -709,6 +736,7 @@ __global__ void __launch_bounds__(512) vq_prefilter_x3(const ConvParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   auto mfmaSub = [&](int u) {
+    __builtin_amdgcn_s_setprio(1);  // keeps the MFMA cluster together (measured +5 %)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -720,6 +748,7 @@ __global__ void __launch_bounds__(512) vq_prefilter_x3(const ConvParams p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[u][i][0]),
                                                             __builtin_bit_cast(bf16x8, fb[u][j][0]), acc[i][j], 0, 0, 0);
       }
+    __builtin_amdgcn_s_setprio(0);
   };
 
   // prologue: steps 0 and 1 staged, step 2 in flight
@@ -778,7 +807,7 @@ template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN>
 static hipError_t launch_x6w8(const ConvParams& p, int batch, int phases, hipStream_t s) {
   const int mtiles = (p.Lq + BM - 1) / BM;
   dim3 grid(mtiles * (p.Cout / BN), batch, phases);
-  hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, WM, WN, HALO, ARGMIN>), grid, dim3(512), 0, s, p);
+  hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, WM, WN, HALO, ARGMIN>), grid, dim3(64 * WM * WN), 0, s, p);
   return hipGetLastError();
 }
 
@@ -790,11 +819,25 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
     const int span = tap_span(p);
     if (span > 64 || (p.Cin / BK) * p.taps % 2) return hipErrorInvalidValue;
     const bool h = span > 0;
-    if (p.Cout % 128 == 0) {
-      if (kname) *kname = h ? "conv_gemm_x6w8<256,128,halo>" : "conv_gemm_x6w8<256,128>";
-      return h ? launch_x6w8<256, 128, 4, 2, 64, false>(p, batch, phases, s)
-               : launch_x6w8<256, 128, 4, 2, 0, false>(p, batch, phases, s);
+    if (p.Cout % 128 == 0 && !h) {  // 1-tap: 4-wave 128 x 128 tiles, two workgroups per CU
+      if (kname) *kname = "conv_gemm_x6w4<128,128>";
+      return launch_x6w8<128, 128, 2, 2, 0, false>(p, batch, phases, s);
     }
+    if (p.Cout % 128 == 0) {
+      if (kname) *kname = "conv_gemm_x6w8<256,128,halo>";
+      return launch_x6w8<256, 128, 4, 2, 64, false>(p, batch, phases, s);
+    }
+#ifndef DCX_SMALLC8
+    // small Cout: 4-wave 256-row tiles (< 80 KB LDS), two workgroups per CU
+    if (p.Cout % 64 == 0) {
+      if (kname) *kname = h ? "conv_gemm_x6w4<256,64,halo>" : "conv_gemm_x6w4<256,64>";
+      return h ? launch_x6w8<256, 64, 4, 1, 64, false>(p, batch, phases, s)
+               : launch_x6w8<256, 64, 4, 1, 0, false>(p, batch, phases, s);
+    }
+    if (kname) *kname = h ? "conv_gemm_x6w4<256,32,halo>" : "conv_gemm_x6w4<256,32>";
+    return h ? launch_x6w8<256, 32, 4, 1, 64, false>(p, batch, phases, s)
+             : launch_x6w8<256, 32, 4, 1, 0, false>(p, batch, phases, s);
+#else
     if (p.Cout % 64 == 0) {
       if (kname) *kname = h ? "conv_gemm_x6w8<512,64,halo>" : "conv_gemm_x6w8<512,64>";
       return h ? launch_x6w8<512, 64, 8, 1, 64, false>(p, batch, phases, s)
@@ -803,6 +846,7 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
     if (kname) *kname = h ? "conv_gemm_x6w8<512,32,halo>" : "conv_gemm_x6w8<512,32>";
     return h ? launch_x6w8<512, 32, 8, 1, 64, false>(p, batch, phases, s)
              : launch_x6w8<512, 32, 8, 1, 0, false>(p, batch, phases, s);
+#endif
   }
   if (p.Cout % 128 == 0) {
     if (kname) *kname = "conv_gemm_f32<128,128>";

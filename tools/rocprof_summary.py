@@ -26,13 +26,10 @@ def short(name):
         return f"{kind}<{parts[0]},{parts[1]}>"
     if base == "vq_prefilter_x3":
         return f"vq_prefilter_x3<{parts[0]},{parts[1]}>"
-    if base == "conv_gemm_x6w8":  # <BM, BN, WM, WN, HALO, ARGMIN, X3>: bench.py's profile names
-        if len(parts) > 6 and parts[6] == "true":
-            return f"vq_prefilter_x3w8<{parts[0]},{parts[1]}>"
-        if parts[5] == "true":
-            return f"vq_dist_argmin_x6w8<{parts[0]},{parts[1]}>"
+    if base == "conv_gemm_x6w8":  # <BM, BN, WM, WN, HALO, ARGMIN>: bench.py's profile names
+        waves = int(parts[2]) * int(parts[3])
         halo = ",halo" if parts[4] != "0" else ""
-        return f"conv_gemm_x6w8<{parts[0]},{parts[1]}{halo}>"
+        return f"conv_gemm_x6w{waves}<{parts[0]},{parts[1]}{halo}>"
     return base + targs.replace(" ", "")
 
 
