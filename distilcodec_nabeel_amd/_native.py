@@ -23,6 +23,7 @@ DCX_ERR_OOM = -5
 DCX_ERR_WORKSPACE = -6
 DCX_GEMM_F32 = 0
 DCX_GEMM_X6 = 1
+DCX_GEMM_BF16 = 2
 
 
 class NativeUnavailable(RuntimeError):

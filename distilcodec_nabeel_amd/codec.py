@@ -7,13 +7,17 @@ kernels on the GPU.  Differences from the reference are listed in DESIGN.md §6;
 
 * the module always computes in eval mode (the reference leaves modules in train mode after
   `from_pretrained`, where EMA would mutate the codebook; README calls `.eval()`);
-* `enable_bfloat16=True` is accepted and computes in fp32 (>= the requested precision);
+* `enable_bfloat16=True` runs the convs / linears in bf16 like the reference's CUDA autocast
+  (engine mode "bf16"), while the mel front end, LayerNorm, residual adds and the VQ distance search
+  stay fp32-accurate (the search returns the exact nearest code of the bf16-valued x_pjt_in).  On the
+  CPU, where the reference's `device_type="cuda"` autocast is inactive, the reference computes fp32;
 * `decode_from_codes_batch` decodes every clip (the reference decodes only clip 0 because of its
   (B,1,L,1) layout -- SURVEY.md §3(C));
 * the mel front end runs on the GPU (the reference forces it to the CPU, mel_spec.py:39).
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 from dataclasses import dataclass, field
@@ -206,6 +210,20 @@ class DistilCodec:
             self._eng = NativeCodec(self.codec_config, self._state, self.device, with_generator=not self.only_quantizer)
         return self._eng
 
+    @contextlib.contextmanager
+    def _precision(self, enable_bfloat16: bool):
+        """torch.autocast(bf16, enabled=enable_bfloat16) of distil_codec.py:550 / 577 / 590 / 621."""
+        eng = self._engine()
+        if not enable_bfloat16 or eng.gemm == "bf16":
+            yield eng
+            return
+        prev = eng.gemm
+        eng.set_gemm("bf16")
+        try:
+            yield eng
+        finally:
+            eng.set_gemm(prev)
+
     # ---------------------------------------------------------------- preprocessing
     def _pad_stack(self, audio_list):
         max_length = max(a.shape[0] for a in audio_list)
@@ -275,13 +293,13 @@ class DistilCodec:
             _, mel_specs, gen_time_lengths, n_hop_lengths = self.preprocess_raw_audio_batch(audio_pathes)
         else:
             _, mel_specs, gen_time_lengths, n_hop_lengths = self.preprocess_audio_batch(audio_pathes)
-        eng = self._engine()
-        feat = eng.encode(_cf(mel_specs))
-        if self.is_debug:
-            print(f"Mel spectrums: {mel_specs.shape}")
-            print(f"Encoded Mel spectrums: {tuple(_cf(feat).shape)}")
         want = not codes_only
-        codes, pin, fup, q = eng.vq_encode(feat, want_pjt_in=want, want_fup=want, want_quantized=want)
+        with self._precision(enable_bfloat16) as eng:
+            feat = eng.encode(_cf(mel_specs))
+            if self.is_debug:
+                print(f"Mel spectrums: {mel_specs.shape}")
+                print(f"Encoded Mel spectrums: {tuple(_cf(feat).shape)}")
+            codes, pin, fup, q = eng.vq_encode(feat, want_pjt_in=want, want_fup=want, want_quantized=want)
         zero = torch.zeros((), device=codes.device)
         ret = GRVQResult(quantized=_cf(q) if q is not None else None, codes=codes.long()[None, :, :, None], codes_list=[],
                          total_loss=zero, commitment_loss=zero.clone(), codebook_diversity_loss=zero.clone(),
@@ -302,7 +320,8 @@ class DistilCodec:
 
     def decode_from_features(self, quantized_features: torch.Tensor, enable_bfloat16: bool = False) -> torch.Tensor:
         """distil_codec.py:575-579."""
-        return self.generator(quantized_features)
+        with self._precision(enable_bfloat16):
+            return self.generator(quantized_features)
 
     def decode_from_codes(self, codes: list, minus_token_offset: bool = True, enable_bfloat16: bool = False) -> torch.Tensor:
         """distil_codec.py:581-594 -> (1, 1, 256 n)."""
@@ -313,8 +332,7 @@ class DistilCodec:
             codes = [c - self.tokens_id_offset for c in codes]
         t = torch.tensor(codes, dtype=torch.int64)[None, :]
         self._check_codes(t)
-        eng = self._engine()
-        with torch.no_grad():
+        with torch.no_grad(), self._precision(enable_bfloat16) as eng:
             z = eng.vq_decode(t)
             wav = eng.generate(z)
         return wav[:, None, :]
@@ -332,8 +350,8 @@ class DistilCodec:
         for i, c in enumerate(codes_list):
             batched[i, : len(c)] = torch.tensor(c, dtype=torch.int64)
         self._check_codes(batched)
-        eng = self._engine()
-        wav = eng.generate(eng.vq_decode(batched))
+        with self._precision(enable_bfloat16) as eng:
+            wav = eng.generate(eng.vq_decode(batched))
         return [wav[i: i + 1, None, :].detach() for i in range(len(codes_list))]
 
     def forward(self, audio_pathes: list):

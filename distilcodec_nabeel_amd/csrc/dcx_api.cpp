@@ -479,7 +479,8 @@ struct CAct {
   CAct(const Act& a) : f(a.f), p(a.p) {}
 };
 
-bool x6_mode(const dcx_codec* h) { return h->gemm_mode == DCX_GEMM_X6; }
+// planes layout for every GEMM operand (x6 and bf16 modes)
+bool x6_mode(const dcx_codec* h) { return h->gemm_mode != DCX_GEMM_F32; }
 
 // Workspace for a tensor consumed only by convs: planes in x6 mode, fp32 otherwise.
 Act conv_input(dcx_codec* h, Bump& ws, size_t n) {
@@ -501,6 +502,7 @@ struct ConvCall {
   const float* res = nullptr;
   const float* gamma = nullptr;
   int epi = dcx::EPI_BIAS, mean = dcx::MEAN_NONE;
+  bool exact = false;  // keep x6 arithmetic in bf16 mode (the reference's fp32 mel front end)
   void silu_to(const Act& a) { y2 = a.f; y6s = a.p; }
   void out_to(const Act& a) { y = a.f; y6 = a.p; }
 };
@@ -536,6 +538,9 @@ int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, boo
   for (int i = 0; i < dcx::kMaxPhases; ++i) p.in_base[i] = w.in_base[i];
   p.epi = c.epi;
   p.mean_mode = c.mean;
+  const bool one = x6 && h->gemm_mode == DCX_GEMM_BF16 && !c.exact;
+  p.nprod = one ? 1 : 6;
+  p.round_bf16 = one;
   ProfScope ps(h, s);
   const char* kname = "conv";
   HIPCHK(h, dcx::launch_conv(p, c.batch, w.phases, s, &kname));
@@ -630,6 +635,7 @@ int stage_mel(dcx_codec* h, const float* audio, int B, int64_t n, Act mel, Bump&
   LAUNCH(h, s, "frame_pad", 0, 8.0 * B * rows * c.hop,
          dcx::launch_frame_pad(audio, fr.f, fr.p, B, n, rows, c.hop, (c.win - c.hop) / 2, s));
   ConvCall cc = framed(fr, B, rows, c.hop);
+  cc.exact = true;
   cc.Lq = T;
   cc.y = spec;
   RUN(run_conv(h, h->dft, cc, s));
@@ -637,6 +643,7 @@ int stage_mel(dcx_codec* h, const float* audio, int B, int64_t n, Act mel, Bump&
   LAUNCH(h, s, "spec_mag", 4.0 * B * T * nbins, 4.0 * B * T * (h->dft.cout + h->melfb.cin),
          dcx::launch_spec_mag(spec, mag.f, mag.p, (long long)B * T, nbins, h->melfb.cin, s));
   ConvCall cm = pointwise(mag, (long long)B * T);
+  cm.exact = true;
   cm.out_to(mel);
   cm.epi = dcx::EPI_LOGCLAMP;
   RUN(run_conv(h, h->melfb, cm, s));
@@ -1161,7 +1168,8 @@ int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int6
 
 int dcx_set_gemm_mode(dcx_codec* h, int32_t mode) {
   if (!h) return DCX_ERR_INVALID_ARG;
-  if (mode != DCX_GEMM_F32 && mode != DCX_GEMM_X6) return fail(h, DCX_ERR_INVALID_ARG, "unknown GEMM mode");
+  if (mode != DCX_GEMM_F32 && mode != DCX_GEMM_X6 && mode != DCX_GEMM_BF16)
+    return fail(h, DCX_ERR_INVALID_ARG, "unknown GEMM mode");
   h->gemm_mode = mode;
   return DCX_OK;
 }
@@ -1218,7 +1226,8 @@ int dcx_conv_forward(dcx_conv* c, int32_t gemm_mode, const float* x, int32_t bat
   h->gemm_mode = gemm_mode;
   hipStream_t s = (hipStream_t)stream;
   CAct xa(x, nullptr);
-  if (gemm_mode == DCX_GEMM_X6) {
+  if (gemm_mode != DCX_GEMM_F32 && gemm_mode != DCX_GEMM_X6 && gemm_mode != DCX_GEMM_BF16) return DCX_ERR_INVALID_ARG;
+  if (gemm_mode != DCX_GEMM_F32) {
     const size_t need = (size_t)batch * lin * c->w.cin * 3;
     if (need > c->planes_cap) {
       if (c->planes) hipFree(c->planes);

@@ -57,6 +57,11 @@ struct XRow {
 };
 
 __device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
+__device__ __forceinline__ f32x4 round_bf16x4(f32x4 v) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = bf16_val(bf16_bits(v[e]));
+  return v;
+}
 __device__ __forceinline__ float gelu_f(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f)); }
 
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
@@ -119,10 +124,12 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, f32x16 (&acc)[
       const long long o = ob + orow * p.ldy + co;
       f32x4 v = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + c4);
       if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + co);
+      if (p.round_bf16) v = round_bf16x4(v);
       switch (p.epi) {
         case EPI_GELU:
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
+          if (p.round_bf16) v = round_bf16x4(v);
           break;
         case EPI_GAMMA_RES:
           v = *reinterpret_cast<const f32x4*>(p.res + o) + *reinterpret_cast<const f32x4*>(p.gamma + co) * v;
@@ -415,13 +422,16 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const ConvParams p) {
 // (two register sets, loop unrolled by two), so a step's MFMAs (2 waves x 24 per SIMD = 1536
 // cycles) cover the L2 / Infinity-Cache latency of the tiles two steps out.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN>
+template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN, int PROD = 6>
 __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams p) {
   static_assert(WM * WN == 8 || WM * WN == 4, "4 or 8 waves per workgroup");
+  static_assert(PROD == 6 || PROD == 1, "x6 or bf16 products");
   constexpr int NT = 64 * WM * WN;
   using XR = XRow<WM * WN == 4>;
   constexpr int XROW = XR::kStride;
-  constexpr int NPC = 6;  // staged 16-byte pieces per row per K chunk
+  // staged 16-byte pieces per row per K chunk: all (half, plane) pairs, or the two hi pieces
+  constexpr int NPC = PROD == 6 ? 6 : 2;
+  constexpr int NPL = PROD == 6 ? 3 : 1;  // planes read into fragments
   constexpr int WR = BM / WM, WC = BN / WN;
   constexpr int TM = WR / 32, TN = WC / 32;
   constexpr int AROWS = BM + HALO;
@@ -458,15 +468,16 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams 
   for (int i = 0; i < A_PT; ++i) {
     const int idx = min(tid + NT * i, A_P - 1);
     a_row[i] = idx / NPC;
-    a_k[i] = idx - a_row[i] * NPC;  // piece = half * 3 + plane
+    a_k[i] = idx - a_row[i] * NPC;
+    if (PROD == 1) a_k[i] *= 3;  // piece = half * 3 + plane
     a_lds[i] = XR::off(a_row[i], a_k[i]);
   }
   int b_off[B_PT], b_lds[B_PT];
 #pragma unroll
   for (int i = 0; i < B_PT; ++i) {
     const int idx = min(tid + NT * i, B_P - 1);
-    const int col = idx / NPC, piece = idx - col * NPC;
-    b_off[i] = idx * 8;
+    const int col = idx / NPC, piece = (idx - col * NPC) * (PROD == 1 ? 3 : 1);
+    b_off[i] = (col * 6 + piece) * 8;
     b_lds[i] = XR::off(col, piece);
   }
 
@@ -521,13 +532,13 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams 
       const int rr = wm * WR + i * 32 + lrow + off;
       const unsigned short* ap = A + rr * XROW + XR::half(rr, khalf) * 24;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const s16x8*>(ap + pl * 8);
+      for (int pl = 0; pl < NPL; ++pl) a[i][pl] = *reinterpret_cast<const s16x8*>(ap + pl * 8);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const unsigned short* bp = Bsm + b_frag[j];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) bb[j][pl] = *reinterpret_cast<const s16x8*>(bp + pl * 8);
+      for (int pl = 0; pl < NPL; ++pl) bb[j][pl] = *reinterpret_cast<const s16x8*>(bp + pl * 8);
     }
   };
 
@@ -597,11 +608,13 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams 
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        DCX_MF(i, j, 2, 0);
-        DCX_MF(i, j, 1, 1);
-        DCX_MF(i, j, 0, 2);
-        DCX_MF(i, j, 1, 0);
-        DCX_MF(i, j, 0, 1);
+        if constexpr (PROD == 6) {
+          DCX_MF(i, j, 2, 0);
+          DCX_MF(i, j, 1, 1);
+          DCX_MF(i, j, 0, 2);
+          DCX_MF(i, j, 1, 0);
+          DCX_MF(i, j, 0, 1);
+        }
         DCX_MF(i, j, 0, 0);
       }
 #undef DCX_MF
@@ -807,7 +820,10 @@ template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN>
 static hipError_t launch_x6w8(const ConvParams& p, int batch, int phases, hipStream_t s) {
   const int mtiles = (p.Lq + BM - 1) / BM;
   dim3 grid(mtiles * (p.Cout / BN), batch, phases);
-  hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, WM, WN, HALO, ARGMIN>), grid, dim3(64 * WM * WN), 0, s, p);
+  if (p.nprod == 1)
+    hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, WM, WN, HALO, ARGMIN, 1>), grid, dim3(64 * WM * WN), 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, WM, WN, HALO, ARGMIN, 6>), grid, dim3(64 * WM * WN), 0, s, p);
   return hipGetLastError();
 }
 
@@ -816,37 +832,37 @@ static int tap_span(const ConvParams& p) { return (p.taps - 1) * (p.in_step < 0 
 hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
   if (p.Cin % BK || p.Cout % 32 || phases < 1 || phases > kMaxPhases) return hipErrorInvalidValue;
   if (p.w6) {
+    if (p.nprod != 6 && p.nprod != 1) return hipErrorInvalidValue;
+    const bool b1 = p.nprod == 1;  // profile names: conv_gemm_bf16w* for the one-product mode
     const int span = tap_span(p);
     if (span > 64 || (p.Cin / BK) * p.taps % 2) return hipErrorInvalidValue;
     const bool h = span > 0;
+    auto name = [&](const char* x6, const char* bf) {
+      if (kname) *kname = b1 ? bf : x6;
+    };
     if (p.Cout % 128 == 0 && !h) {  // 1-tap: 4-wave 128 x 128 tiles, two workgroups per CU
-      if (kname) *kname = "conv_gemm_x6w4<128,128>";
+      name("conv_gemm_x6w4<128,128>", "conv_gemm_bf16w4<128,128>");
       return launch_x6w8<128, 128, 2, 2, 0, false>(p, batch, phases, s);
     }
     if (p.Cout % 128 == 0) {
-      if (kname) *kname = "conv_gemm_x6w8<256,128,halo>";
+      name("conv_gemm_x6w8<256,128,halo>", "conv_gemm_bf16w8<256,128,halo>");
       return launch_x6w8<256, 128, 4, 2, 64, false>(p, batch, phases, s);
     }
-#ifndef DCX_SMALLC8
     // small Cout: 4-wave 256-row tiles (< 80 KB LDS), two workgroups per CU
     if (p.Cout % 64 == 0) {
-      if (kname) *kname = h ? "conv_gemm_x6w4<256,64,halo>" : "conv_gemm_x6w4<256,64>";
-      return h ? launch_x6w8<256, 64, 4, 1, 64, false>(p, batch, phases, s)
-               : launch_x6w8<256, 64, 4, 1, 0, false>(p, batch, phases, s);
+      if (h) {
+        name("conv_gemm_x6w4<256,64,halo>", "conv_gemm_bf16w4<256,64,halo>");
+        return launch_x6w8<256, 64, 4, 1, 64, false>(p, batch, phases, s);
+      }
+      name("conv_gemm_x6w4<256,64>", "conv_gemm_bf16w4<256,64>");
+      return launch_x6w8<256, 64, 4, 1, 0, false>(p, batch, phases, s);
     }
-    if (kname) *kname = h ? "conv_gemm_x6w4<256,32,halo>" : "conv_gemm_x6w4<256,32>";
-    return h ? launch_x6w8<256, 32, 4, 1, 64, false>(p, batch, phases, s)
-             : launch_x6w8<256, 32, 4, 1, 0, false>(p, batch, phases, s);
-#else
-    if (p.Cout % 64 == 0) {
-      if (kname) *kname = h ? "conv_gemm_x6w8<512,64,halo>" : "conv_gemm_x6w8<512,64>";
-      return h ? launch_x6w8<512, 64, 8, 1, 64, false>(p, batch, phases, s)
-               : launch_x6w8<512, 64, 8, 1, 0, false>(p, batch, phases, s);
+    if (h) {
+      name("conv_gemm_x6w4<256,32,halo>", "conv_gemm_bf16w4<256,32,halo>");
+      return launch_x6w8<256, 32, 4, 1, 64, false>(p, batch, phases, s);
     }
-    if (kname) *kname = h ? "conv_gemm_x6w8<512,32,halo>" : "conv_gemm_x6w8<512,32>";
-    return h ? launch_x6w8<512, 32, 8, 1, 64, false>(p, batch, phases, s)
-             : launch_x6w8<512, 32, 8, 1, 0, false>(p, batch, phases, s);
-#endif
+    name("conv_gemm_x6w4<256,32>", "conv_gemm_bf16w4<256,32>");
+    return launch_x6w8<256, 32, 4, 1, 0, false>(p, batch, phases, s);
   }
   if (p.Cout % 128 == 0) {
     if (kname) *kname = "conv_gemm_f32<128,128>";

@@ -51,6 +51,9 @@ struct ConvParams {
   float* part_val;      // [rows][ntiles]
   int* part_idx;        // [rows][ntiles]
   float* part_val2;     // [rows][ntiles] second-smallest value (VQ prefilter)
+  // planes-mode arithmetic: 6 = x6 (fp32-accurate), 1 = bf16 (hi plane only, one product);
+  // round_bf16: round the GEMM result (after bias, and after GELU) to bf16 like torch.autocast
+  int nprod, round_bf16;
 };
 
 // Launchers (all stream-ordered, no allocation).  Return hipError_t of the launch.

@@ -15,12 +15,14 @@ from . import _native
 from .config import check_supported
 
 
-GEMM_MODES = {"f32": _native.DCX_GEMM_F32, "x6": _native.DCX_GEMM_X6}
+GEMM_MODES = {"f32": _native.DCX_GEMM_F32, "x6": _native.DCX_GEMM_X6, "bf16": _native.DCX_GEMM_BF16}
 
 
 class NativeCodec:
     """`gemm`: "x6" (default; fp32 operands as three bf16 planes, six exact products, fp32
-    accumulation) or "f32" (v_mfma_f32_32x32x2_f32).  Env DCX_GEMM overrides the default."""
+    accumulation), "f32" (v_mfma_f32_32x32x2_f32) or "bf16" (the reference's enable_bfloat16:
+    bf16 operands and results, fp32 accumulation; see DCX_GEMM_BF16).  Env DCX_GEMM overrides
+    the default."""
 
     def __init__(self, cfg: dict, state: dict, device, with_generator: bool = True, gemm: str | None = None):
         check_supported(cfg)

@@ -129,10 +129,16 @@ int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int6
 /* Arithmetic of every contraction (convs, linears, STFT, mel, VQ distances):
  *  DCX_GEMM_X6  (default) fp32 operands split into three bf16 planes, six exact bf16 products per
  *               fp32 product, fp32 accumulation on v_mfma_f32_32x32x16_bf16 (fp32-level accuracy);
- *  DCX_GEMM_F32 v_mfma_f32_32x32x2_f32 (IEEE fp32 fma chain).
- * May be changed at any time; the VQ decode table keeps the mode active at dcx_finalize. */
+ *  DCX_GEMM_F32 v_mfma_f32_32x32x2_f32 (IEEE fp32 fma chain);
+ *  DCX_GEMM_BF16 the reference's enable_bfloat16 (torch.autocast bf16, distil_codec.py:550): conv /
+ *               linear operands rounded to bf16, one bf16 product, fp32 accumulation, results
+ *               rounded to bf16 (after bias, and after GELU); LayerNorm, residual adds and the mel
+ *               front end (computed before autocast in the reference) stay fp32-accurate, and the
+ *               VQ search stays exact (prefilter + fp64 rescore) on the bf16-valued x_pjt_in.
+ * May be changed at any time; the VQ decode table is always built in fp32 at dcx_finalize. */
 #define DCX_GEMM_F32 0
 #define DCX_GEMM_X6 1
+#define DCX_GEMM_BF16 2
 int dcx_set_gemm_mode(dcx_codec* h, int32_t mode);
 int32_t dcx_get_gemm_mode(const dcx_codec* h);
 

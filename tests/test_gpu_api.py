@@ -96,8 +96,10 @@ def test_path_input_and_demo(codec, tmp_path):
     r_path, _, hop = codec.encode([p])
     r_raw, _, _ = codec.encode([[xq, 24000]], raw_audio=True)
     assert torch.equal(r_path.codes, r_raw.codes) and hop == [36000 // 256]
-    toks = demo_for_generate_audio_codes(codec, p)
-    assert toks == (r_raw.codes.squeeze().cpu() + codec.tokens_id_offset).tolist()
+    toks = demo_for_generate_audio_codes(codec, p)  # encodes with enable_bfloat16=True, like the reference
+    r_bf, _, _ = codec.encode([[xq, 24000]], enable_bfloat16=True, raw_audio=True)
+    assert toks == (r_bf.codes.squeeze().cpu() + codec.tokens_id_offset).tolist()
+    assert codec._engine().gemm == "x6"  # the bf16 context restores the default mode
     # unreadable file: the reference substitutes 1 s of N(0,1)*0.05 noise (distil_codec.py:155-160)
     r_bad, _, hop_bad = codec.encode([str(tmp_path / "missing.wav")])
     assert hop_bad == [24000 // 256] and r_bad.codes.shape[2] == 93
