@@ -716,7 +716,8 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
     ProfScope ps(h, s);
     const char* kname = "vq";
     if (x6) {
-      HIPCHK(h, dcx::launch_vq_prefilter(p, (int)M, s, &kname));
+      // bf16 mode rounds x_pjt_in to bf16 in the project_in epilogue (round_bf16)
+      HIPCHK(h, dcx::launch_vq_prefilter(p, (int)M, h->gemm_mode == DCX_GEMM_BF16, s, &kname));
       ps.done(kname, 2.0 * M * NC * CD, 4.0 * ((double)M * CD + (double)NC * CD));
     } else {
       HIPCHK(h, dcx::launch_vq_argmin(p, (int)M, s, &kname));

@@ -651,14 +651,17 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams 
 // sub-chunk 1 of step s is on the matrix cores, and vice versa.  Loads run three steps ahead
 // (input tile double buffer, weight ring of 3), stores two.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN>
+// XMID = false: the rows of x are bf16 values (mid plane zero, bf16 mode), so only their hi pieces
+// are staged and hi*hi + hi*mid' issued (2 products; the bound of launch_vq_prefilter still holds).
+template <int BM, int BN, int WM, int WN, bool XMID>
 __global__ void __launch_bounds__(512) vq_prefilter_x3(const ConvParams p) {
   static_assert(WM * WN == 8, "8 waves per workgroup");
   constexpr int WR = BM / WM, WC = BN / WN;
   constexpr int TM = WR / 32, TN = WC / 32;
   constexpr int ROW = 72;  // ushort per LDS row: 8 pieces + 1 pad piece
-  constexpr int A_PT = BM * 8 / 512, B_PT = BN * 8 / 512;
-  static_assert(BM * 8 % 512 == 0 && BN * 8 % 512 == 0, "staging pieces per thread");
+  constexpr int APC = XMID ? 8 : 4;  // staged pieces per input row per step
+  constexpr int A_PT = BM * APC / 512, B_PT = BN * 8 / 512;
+  static_assert(BM * APC % 512 == 0 && BN * 8 % 512 == 0, "staging pieces per thread");
   constexpr int ABUF = BM * ROW, BBUF = BN * ROW;
   __shared__ __attribute__((aligned(16))) unsigned short lds[2 * ABUF + 3 * BBUF];
 
@@ -682,7 +685,7 @@ __global__ void __launch_bounds__(512) vq_prefilter_x3(const ConvParams p) {
   int a_lds[A_PT];
 #pragma unroll
   for (int i = 0; i < A_PT; ++i) {
-    const int idx = tid + 512 * i, row = idx >> 3, k = idx & 7;
+    const int idx = tid + 512 * i, row = idx / APC, k = XMID ? idx & 7 : (idx & 3) * 2;  // hi pieces only
     const int q = q0 + row;
     const int goff = (k >> 2) * 48 + ((k >> 1) & 1) * 24 + (k & 1) * 8;
     a_src[i] = q < p.Lq ? p.x6 + (long long)q * ldx6 + goff : reinterpret_cast<const unsigned short*>(g_zero_row);
@@ -691,7 +694,7 @@ __global__ void __launch_bounds__(512) vq_prefilter_x3(const ConvParams p) {
   const int a_step = 96;  // ushort per step along a row (zero-page rows must not advance)
   bool a_live[A_PT];
 #pragma unroll
-  for (int i = 0; i < A_PT; ++i) a_live[i] = q0 + ((tid + 512 * i) >> 3) < p.Lq;
+  for (int i = 0; i < A_PT; ++i) a_live[i] = q0 + (tid + 512 * i) / APC < p.Lq;
   long long b_off[B_PT];
   int b_lds[B_PT];
 #pragma unroll
@@ -731,7 +734,7 @@ __global__ void __launch_bounds__(512) vq_prefilter_x3(const ConvParams p) {
     for (int i = 0; i < TM; ++i) {
       const unsigned short* ap = A + (wm * WR + i * 32 + lrow) * ROW;
       fa[u][i][0] = *reinterpret_cast<const s16x8*>(ap);
-      fa[u][i][1] = *reinterpret_cast<const s16x8*>(ap + 8);
+      if constexpr (XMID) fa[u][i][1] = *reinterpret_cast<const s16x8*>(ap + 8);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -754,8 +757,9 @@ __global__ void __launch_bounds__(512) vq_prefilter_x3(const ConvParams p) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[u][i][1]),
-                                                            __builtin_bit_cast(bf16x8, fb[u][j][0]), acc[i][j], 0, 0, 0);
+        if constexpr (XMID)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[u][i][1]),
+                                                              __builtin_bit_cast(bf16x8, fb[u][j][0]), acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[u][i][0]),
                                                             __builtin_bit_cast(bf16x8, fb[u][j][1]), acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[u][i][0]),
@@ -894,7 +898,7 @@ hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const 
 // roundings per MFMA).  By Cauchy-Schwarz sum_k |x_k e_k| <= |x| max|e|, so each approximate
 // squared distance is within 2 * kVqPrefilterBound * |x| max|e| + 8 * 2^-24 (|x|^2 + max|e|^2)
 // of the exact one; vq_rescore_kernel uses that bound.
-hipError_t launch_vq_prefilter(const ConvParams& p, int rows, hipStream_t s, const char** kname) {
+hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipStream_t s, const char** kname) {
   constexpr int BM = 256, BN = 128;
   if (!p.w6 || !p.x6 || !p.part_val2 || p.Cin % BK || p.Cout % (BN * 16) || rows < 1) return hipErrorInvalidValue;
   ConvParams q = p;
@@ -905,8 +909,13 @@ hipError_t launch_vq_prefilter(const ConvParams& p, int rows, hipStream_t s, con
   const int nsm = (mtiles + 15) / 16;
   dim3 grid((unsigned)(nsm * (ntiles / 16) * 256));
   if (p.Cin % 64) return hipErrorInvalidValue;  // even number of K32 steps
-  if (kname) *kname = "vq_prefilter_x3<256,128>";
-  hipLaunchKernelGGL((vq_prefilter_x3<BM, BN, 4, 2>), grid, dim3(512), 0, s, q);
+  if (x_bf16) {
+    if (kname) *kname = "vq_prefilter_x2<256,128>";
+    hipLaunchKernelGGL((vq_prefilter_x3<BM, BN, 4, 2, false>), grid, dim3(512), 0, s, q);
+  } else {
+    if (kname) *kname = "vq_prefilter_x3<256,128>";
+    hipLaunchKernelGGL((vq_prefilter_x3<BM, BN, 4, 2, true>), grid, dim3(512), 0, s, q);
+  }
   return hipGetLastError();
 }
 

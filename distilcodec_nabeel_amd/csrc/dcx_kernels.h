@@ -61,7 +61,8 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname);
 int vq_argmin_ntiles(int ncodes);
 // VQ search, x6 mode: bf16x3 prefilter (approximate squared distances, per-tile top 2) ...
-hipError_t launch_vq_prefilter(const ConvParams& p, int rows, hipStream_t s, const char** kname);
+// x_bf16: the rows of x are bf16 values (mid and lo planes zero), which drops the mid*hi product.
+hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipStream_t s, const char** kname);
 // ... then per row: certify the prefilter's winner with a rigorous error bound, or rescore every
 // candidate inside the bound in fp64.  stats (optional): [0] rows rescored, [1] codes rescored.
 constexpr float kVqPrefilterBound = 2.5e-4f;

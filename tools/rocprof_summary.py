@@ -25,7 +25,8 @@ def short(name):
         kind = "vq_dist_argmin_f32" if parts[-1] == "true" else "conv_gemm_f32"
         return f"{kind}<{parts[0]},{parts[1]}>"
     if base == "vq_prefilter_x3":
-        return f"vq_prefilter_x3<{parts[0]},{parts[1]}>"
+        kind = "vq_prefilter_x3" if len(parts) < 5 or parts[4] == "true" else "vq_prefilter_x2"
+        return f"{kind}<{parts[0]},{parts[1]}>"
     if base == "conv_gemm_x6w8":  # <BM, BN, WM, WN, HALO, ARGMIN>: bench.py's profile names
         waves = int(parts[2]) * int(parts[3])
         halo = ",halo" if parts[4] != "0" else ""
