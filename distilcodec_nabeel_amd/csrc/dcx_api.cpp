@@ -507,9 +507,14 @@ struct ConvCall {
   void out_to(const Act& a) { y = a.f; y6 = a.p; }
 };
 
+// Planes-mode convs with Cin <= 64 and a tap halo may take an fp32 input (split while staging).
+bool f32_input_ok(const ConvW& w) { return w.cin <= 64 && w.cout <= 64 && w.taps >= 2; }
+
 int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, bool force_f32 = false) {
   const bool x6 = x6_mode(h) && !force_f32;
-  if (x6 ? (!c.x.p || !w.w6) : !c.x.f) return fail(h, DCX_ERR_STATE, "internal: conv input missing for GEMM mode");
+  const bool x6_f32in = x6 && !c.x.p && c.x.f && f32_input_ok(w);
+  if (x6 ? ((!c.x.p && !x6_f32in) || !w.w6) : !c.x.f)
+    return fail(h, DCX_ERR_STATE, "internal: conv input missing for GEMM mode");
   ConvParams p{};
   p.x = c.x.f;
   p.x6 = x6 ? c.x.p : nullptr;
@@ -783,6 +788,12 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
   Act Tb = conv_input(h, ws, per);  // silu(c1 output)
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for generate");
+  // Tensors consumed by Cin <= 64 convs are kept in fp32 (the kernels split them while staging):
+  // those stages are bound by HBM traffic, and planes cost 6 B per element against 4.
+  auto in_form = [&](const Act& a, int consumer_cin) -> Act {
+    if (!x6_mode(h) || consumer_cin > 64) return a;
+    return Act{a.f ? a.f : reinterpret_cast<float*>(a.p), nullptr};
+  };
   int C = c.gen_channels, L = T;
   {  // conv_pre, then the first stage's SiLU (generators.py:121,125) fused as the only output
     ConvCall cc = framed(z, B, T, c.vq_dim);
@@ -792,35 +803,36 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
   for (int i = 0; i < c.n_ups; ++i) {
     const ConvW& up = h->ups[i];
     const int Co = up.cout, Lo = L * c.up_rates[i];
+    const Act S_i = in_form(S, C), XS_i = in_form(XS, Co), RS_i = in_form(RS, Co), Tb_i = in_form(Tb, Co);
     {
-      ConvCall cc = framed(S, B, L, C);
+      ConvCall cc = framed(S_i, B, L, C);
       cc.y = X;
-      cc.silu_to(XS);
+      cc.silu_to(XS_i);
       RUN(run_conv(h, up, cc, s));
     }
     const bool last_stage = i == c.n_ups - 1;
     for (int rb = 0; rb < c.n_res; ++rb) {
       for (int ci = 0; ci < 3; ++ci) {
-        const Act& src = ci == 0 ? XS : RS;
+        const Act& src = ci == 0 ? XS_i : RS_i;
         const float* resid = ci == 0 ? X : R;
         {
           ConvCall cc = framed(src, B, Lo, Co);
-          cc.silu_to(Tb);
+          cc.silu_to(Tb_i);
           RUN(run_conv(h, h->res[i][rb][ci][0], cc, s));
         }
-        ConvCall cc = framed(Tb, B, Lo, Co);
+        ConvCall cc = framed(Tb_i, B, Lo, Co);
         cc.epi = dcx::EPI_RES;
         cc.res = resid;
         if (ci < 2) {
           cc.y = R;
-          cc.silu_to(RS);
+          cc.silu_to(RS_i);
         } else {
           cc.macc = Mx;
           cc.mean = rb == 0 ? dcx::MEAN_FIRST : (rb == c.n_res - 1 ? dcx::MEAN_LAST : dcx::MEAN_MID);
           if (rb == c.n_res - 1) {
             // silu(mean): input of ups[i+1], or (fp32, in place) of conv_post
             if (last_stage) cc.y2 = Mx;
-            else cc.silu_to(S);
+            else cc.silu_to(in_form(S, Co));  // the next ConvT reads it with Cin = Co
           }
         }
         RUN(run_conv(h, h->res[i][rb][ci][1], cc, s));
@@ -1228,7 +1240,7 @@ int dcx_conv_forward(dcx_conv* c, int32_t gemm_mode, const float* x, int32_t bat
   hipStream_t s = (hipStream_t)stream;
   CAct xa(x, nullptr);
   if (gemm_mode != DCX_GEMM_F32 && gemm_mode != DCX_GEMM_X6 && gemm_mode != DCX_GEMM_BF16) return DCX_ERR_INVALID_ARG;
-  if (gemm_mode != DCX_GEMM_F32) {
+  if (gemm_mode != DCX_GEMM_F32 && !f32_input_ok(c->w)) {
     const size_t need = (size_t)batch * lin * c->w.cin * 3;
     if (need > c->planes_cap) {
       if (c->planes) hipFree(c->planes);

@@ -422,7 +422,10 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const ConvParams p) {
 // (two register sets, loop unrolled by two), so a step's MFMAs (2 waves x 24 per SIMD = 1536
 // cycles) cover the L2 / Infinity-Cache latency of the tiles two steps out.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN, int PROD = 6>
+// AF32: the input is fp32 (p.x6 == nullptr) and is split into planes while staging (4 channels
+// per 16-byte load, three 8-byte LDS stores).  Used for Cin <= 64, where the convs are bound by
+// HBM traffic and planes (6 B per element) would cost 1.5x the fp32 bytes.
+template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN, int PROD = 6, bool AF32 = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams p) {
   static_assert(WM * WN == 8 || WM * WN == 4, "4 or 8 waves per workgroup");
   static_assert(PROD == 6 || PROD == 1, "x6 or bf16 products");
@@ -432,10 +435,11 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams 
   // staged 16-byte pieces per row per K chunk: all (half, plane) pairs, or the two hi pieces
   constexpr int NPC = PROD == 6 ? 6 : 2;
   constexpr int NPL = PROD == 6 ? 3 : 1;  // planes read into fragments
+  constexpr int APC = AF32 ? 4 : NPC;     // staged 16-byte pieces per input row per K chunk
   constexpr int WR = BM / WM, WC = BN / WN;
   constexpr int TM = WR / 32, TN = WC / 32;
   constexpr int AROWS = BM + HALO;
-  constexpr int A_P = AROWS * NPC;  // 16-byte pieces of a staged input tile (planes)
+  constexpr int A_P = AROWS * APC;  // 16-byte pieces of a staged input tile
   constexpr int B_P = BN * NPC;
   constexpr int A_PT = (A_P + NT - 1) / NT, B_PT = (B_P + NT - 1) / NT;
   constexpr int ABUF = AROWS * XROW, BBUF = BN * XROW;
@@ -450,7 +454,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams 
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
   const int b = blockIdx.y, ph = blockIdx.z;
-  const unsigned short* __restrict__ xb6 = p.x6 + (long long)b * p.x_bstride * 3;
+  const unsigned short* __restrict__ xb6 = AF32 ? nullptr : p.x6 + (long long)b * p.x_bstride * 3;
+  const float* __restrict__ xbf = AF32 ? p.x + (long long)b * p.x_bstride : nullptr;
   const long long ldx6 = (long long)p.ldx * 3;
   const int nchunks = p.Cin / BK;
   const int taps = p.taps;
@@ -467,10 +472,14 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams 
 #pragma unroll
   for (int i = 0; i < A_PT; ++i) {
     const int idx = min(tid + NT * i, A_P - 1);
-    a_row[i] = idx / NPC;
-    a_k[i] = idx - a_row[i] * NPC;
-    if (PROD == 1) a_k[i] *= 3;  // piece = half * 3 + plane
-    a_lds[i] = XR::off(a_row[i], a_k[i]);
+    a_row[i] = idx / APC;
+    a_k[i] = idx - a_row[i] * APC;
+    if constexpr (AF32) {  // a_k = 4-channel group; LDS: its half's hi plane + (a_k & 1) * 4
+      a_lds[i] = XR::off(a_row[i], (a_k[i] >> 1) * 3) + (a_k[i] & 1) * 4;
+    } else {
+      if (PROD == 1) a_k[i] *= 3;  // piece = half * 3 + plane
+      a_lds[i] = XR::off(a_row[i], a_k[i]);
+    }
   }
   int b_off[B_PT], b_lds[B_PT];
 #pragma unroll
@@ -492,15 +501,39 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams 
     for (int i = 0; i < A_PT; ++i) {
       const int ir = row0 + a_row[i];
       const bool ok = ir >= 0 && ir < lin;
-      const unsigned short* src =
-          ok ? xb6 + (long long)ir * ldx6 + c * 48 + a_k[i] * 8 : reinterpret_cast<const unsigned short*>(g_zero_row);
-      r[i] = *reinterpret_cast<const f32x4*>(src);
+      if constexpr (AF32) {
+        const float* src = ok ? xbf + (long long)ir * p.ldx + c * 16 + a_k[i] * 4 : g_zero_row;
+        r[i] = *reinterpret_cast<const f32x4*>(src);
+      } else {
+        const unsigned short* src =
+            ok ? xb6 + (long long)ir * ldx6 + c * 48 + a_k[i] * 8 : reinterpret_cast<const unsigned short*>(g_zero_row);
+        r[i] = *reinterpret_cast<const f32x4*>(src);
+      }
     }
   };
   auto storeA = [&](int buf, const f32x4(&r)[A_PT]) {
     unsigned short* A = lds + buf * ABUF;
 #pragma unroll
-    for (int i = 0; i < A_PT; ++i) *reinterpret_cast<f32x4*>(A + a_lds[i]) = r[i];
+    for (int i = 0; i < A_PT; ++i) {
+      if constexpr (AF32) {
+        s16x4 hv, mv, lv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          unsigned short hb, mb, lb;
+          split3(r[i][e], hb, mb, lb);
+          hv[e] = (short)hb;
+          mv[e] = (short)mb;
+          lv[e] = (short)lb;
+        }
+        *reinterpret_cast<s16x4*>(A + a_lds[i]) = hv;
+        if constexpr (PROD == 6) {
+          *reinterpret_cast<s16x4*>(A + a_lds[i] + 8) = mv;
+          *reinterpret_cast<s16x4*>(A + a_lds[i] + 16) = lv;
+        }
+      } else {
+        *reinterpret_cast<f32x4*>(A + a_lds[i]) = r[i];
+      }
+    }
   };
   auto loadB = [&](int c, int m, f32x4(&r)[B_PT]) {
     const unsigned short* src = wbase + ((long long)m * nchunks + c) * wslab;
@@ -831,6 +864,18 @@ static hipError_t launch_x6w8(const ConvParams& p, int batch, int phases, hipStr
   return hipGetLastError();
 }
 
+// fp32-input variant (Cin <= 64 convs, see conv_gemm_x6w8)
+template <int BM, int BN, int WM, int WN, int HALO>
+static hipError_t launch_x6w8_af32(const ConvParams& p, int batch, int phases, hipStream_t s) {
+  const int mtiles = (p.Lq + BM - 1) / BM;
+  dim3 grid(mtiles * (p.Cout / BN), batch, phases);
+  if (p.nprod == 1)
+    hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, WM, WN, HALO, false, 1, true>), grid, dim3(64 * WM * WN), 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, WM, WN, HALO, false, 6, true>), grid, dim3(64 * WM * WN), 0, s, p);
+  return hipGetLastError();
+}
+
 static int tap_span(const ConvParams& p) { return (p.taps - 1) * (p.in_step < 0 ? -p.in_step : p.in_step); }
 
 hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
@@ -844,6 +889,15 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
     auto name = [&](const char* x6, const char* bf) {
       if (kname) *kname = b1 ? bf : x6;
     };
+    if (!p.x6) {  // fp32 input, split while staging: small-Cout tiles only
+      if (!p.x || p.Cin > 64 || p.Cout > 64 || p.taps < 2) return hipErrorInvalidValue;
+      if (p.Cout == 64) {
+        name("conv_gemm_x6w4f<256,64,halo>", "conv_gemm_bf16w4f<256,64,halo>");
+        return launch_x6w8_af32<256, 64, 4, 1, 64>(p, batch, phases, s);
+      }
+      name("conv_gemm_x6w4f<256,32,halo>", "conv_gemm_bf16w4f<256,32,halo>");
+      return launch_x6w8_af32<256, 32, 4, 1, 64>(p, batch, phases, s);
+    }
     if (p.Cout % 128 == 0 && !h) {  // 1-tap: 4-wave 128 x 128 tiles, two workgroups per CU
       name("conv_gemm_x6w4<128,128>", "conv_gemm_bf16w4<128,128>");
       return launch_x6w8<128, 128, 2, 2, 0, false>(p, batch, phases, s);

@@ -19,6 +19,10 @@ SHAPES = {  # name: (cin, cout, k, dil, transposed, stride, B, L)
     "res128_k11": (128, 128, 11, 1, False, 1, 32, 64 * T),
     "res64_k7d3": (64, 64, 7, 3, False, 1, 32, 128 * T),
     "res32_k11d5": (32, 32, 11, 5, False, 1, 32, 256 * T),
+    "res32_k7d3": (32, 32, 7, 3, False, 1, 32, 256 * T),
+    "res32_k3d1": (32, 32, 3, 1, False, 1, 32, 256 * T),
+    "res64_k3d1": (64, 64, 3, 1, False, 1, 32, 128 * T),
+    "res64_k11d5": (64, 64, 11, 5, False, 1, 32, 128 * T),
     "ups0": (1024, 512, 16, 1, True, 8, 32, T),
     "pw1_1024": (1024, 4096, 1, 1, False, 1, 1, 32 * T),
     "pw2_1024": (4096, 1024, 1, 1, False, 1, 1, 32 * T),
