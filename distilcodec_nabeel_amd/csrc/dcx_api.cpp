@@ -507,8 +507,9 @@ struct ConvCall {
   void out_to(const Act& a) { y = a.f; y6 = a.p; }
 };
 
-// Planes-mode convs with Cin <= 64 and a tap halo may take an fp32 input (split while staging).
-bool f32_input_ok(const ConvW& w) { return w.cin <= 64 && w.cout <= 64 && w.taps >= 2; }
+// Planes-mode convs with Cout <= 64, Cin <= 128 and a tap halo take an fp32 input (split while
+// staging; conv_gemm_x6w8 AF32).
+bool f32_input_ok(const ConvW& w) { return w.cin <= 128 && w.cout <= 64 && w.taps >= 2; }
 
 int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, bool force_f32 = false) {
   const bool x6 = x6_mode(h) && !force_f32;
@@ -788,10 +789,10 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
   Act Tb = conv_input(h, ws, per);  // silu(c1 output)
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for generate");
-  // Tensors consumed by Cin <= 64 convs are kept in fp32 (the kernels split them while staging):
-  // those stages are bound by HBM traffic, and planes cost 6 B per element against 4.
-  auto in_form = [&](const Act& a, int consumer_cin) -> Act {
-    if (!x6_mode(h) || consumer_cin > 64) return a;
+  // Tensors consumed by small-Cout convs are kept in fp32 (those kernels split them while
+  // staging: the stages are bound by HBM traffic, and planes cost 6 B per element against 4).
+  auto in_form = [&](const Act& a, const ConvW& consumer) -> Act {
+    if (!x6_mode(h) || !f32_input_ok(consumer)) return a;
     return Act{a.f ? a.f : reinterpret_cast<float*>(a.p), nullptr};
   };
   int C = c.gen_channels, L = T;
@@ -803,7 +804,8 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
   for (int i = 0; i < c.n_ups; ++i) {
     const ConvW& up = h->ups[i];
     const int Co = up.cout, Lo = L * c.up_rates[i];
-    const Act S_i = in_form(S, C), XS_i = in_form(XS, Co), RS_i = in_form(RS, Co), Tb_i = in_form(Tb, Co);
+    const ConvW& rconv = h->res[i][0][0][0];  // every ResBlock conv of the stage has Cin = Cout = Co
+    const Act S_i = in_form(S, up), XS_i = in_form(XS, rconv), RS_i = in_form(RS, rconv), Tb_i = in_form(Tb, rconv);
     {
       ConvCall cc = framed(S_i, B, L, C);
       cc.y = X;
@@ -832,7 +834,7 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
           if (rb == c.n_res - 1) {
             // silu(mean): input of ups[i+1], or (fp32, in place) of conv_post
             if (last_stage) cc.y2 = Mx;
-            else cc.silu_to(in_form(S, Co));  // the next ConvT reads it with Cin = Co
+            else cc.silu_to(in_form(S, h->ups[i + 1]));  // input of the next ConvT
           }
         }
         RUN(run_conv(h, h->res[i][rb][ci][1], cc, s));

@@ -24,6 +24,7 @@
 // MFMA fragment maps (cdna_hip_programming.md §3): 32x32x2 f32: lane l supplies A[l&31][k=l>>5]
 // and B[k=l>>5][l&31]; 32x32x16 bf16: A[l&31][k=8(l>>5)+j], B[k=8(l>>5)+j][l&31], j<8;
 // C/D for both: col=l&31, row=(r&3)+8*(r>>2)+4*(l>>5).
+#include <algorithm>
 #include <type_traits>
 
 #include "dcx_kernels.h"
@@ -76,6 +77,20 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // instead of the loaded value keeps every staging load unconditional, so hipcc neither branches
 // around it nor waits vmcnt(0) after it (cdna_hip_programming.md §5, trap 4(c)).
 __device__ __attribute__((aligned(16))) float g_zero_row[32] = {0.f};
+
+#ifdef DCX_CLOCK_DIAG
+// Diagnostic build only: per-workgroup shader-clock and 100 MHz real-time ticks over the main
+// loop, summed (in-kernel clock = sum(memtime) / sum(realtime) * 100 MHz).
+__device__ unsigned long long g_clock_diag[3];
+extern "C" int dcx_diag_clock(unsigned long long* out3, int reset) {
+  if (hipMemcpyFromSymbol(out3, HIP_SYMBOL(g_clock_diag), sizeof(unsigned long long) * 3) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned long long z[3] = {0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_clock_diag), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // Conv epilogue through LDS: the accumulator tile is written to LDS (in row passes that fit the
@@ -423,10 +438,11 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const ConvParams p) {
 // cycles) cover the L2 / Infinity-Cache latency of the tiles two steps out.
 // ---------------------------------------------------------------------------------------------
 // AF32: the input is fp32 (p.x6 == nullptr) and is split into planes while staging (4 channels
-// per 16-byte load, three 8-byte LDS stores).  Used for Cin <= 64, where the convs are bound by
-// HBM traffic and planes (6 B per element) would cost 1.5x the fp32 bytes.
+// per 16-byte load, three 8-byte LDS stores).  Used for the small-Cout convs (Cout <= 64, Cin <= 128),
+// which are bound by HBM traffic (planes cost 6 B per element against 4) and whose planes-input
+// variant would need more than 256 VGPRs.
 template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN, int PROD = 6, bool AF32 = false>
-__global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams p) {
+__global__ void __launch_bounds__(64 * WM * WN, 2) conv_gemm_x6w8(const ConvParams p) {
   static_assert(WM * WN == 8 || WM * WN == 4, "4 or 8 waves per workgroup");
   static_assert(PROD == 6 || PROD == 1, "x6 or bf16 products");
   constexpr int NT = 64 * WM * WN;
@@ -447,25 +463,46 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams 
   // LDS: input tiles (2, by chunk parity) + weight-tile ring (3, by step mod 3).
   __shared__ __attribute__((aligned(16))) unsigned short lds[2 * ABUF + 3 * BBUF];
 
+  static_assert(!ARGMIN, "x6 VQ search uses vq_prefilter_x3");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int ntiles = p.Cout / BN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int mt = wg / ntiles, nt = wg - mt * ntiles;
-  const int q0 = mt * BM, co0 = nt * BN;
-  const int b = blockIdx.y, ph = blockIdx.z;
-  const unsigned short* __restrict__ xb6 = AF32 ? nullptr : p.x6 + (long long)b * p.x_bstride * 3;
-  const float* __restrict__ xbf = AF32 ? p.x + (long long)b * p.x_bstride : nullptr;
   const long long ldx6 = (long long)p.ldx * 3;
   const int nchunks = p.Cin / BK;
   const int taps = p.taps;
   const int nsteps = nchunks * taps;
   const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
-  const int row0 = q0 + p.in_base[ph] + lo_rel;
-  const unsigned short* __restrict__ wbase =
-      p.w6 + ((long long)ph * taps * nchunks) * p.Cout * 48 + (long long)co0 * 48;
   const long long wslab = (long long)p.Cout * 48;
   const int lin = p.Lin;
+
+  // Persistent tiles.  Iteration `it` of block w takes logical tile
+  //   it * G + (w & 7) * (G / 8) + (w >> 3)      (G = gridDim.x, a multiple of 8)
+  // so the blocks of one XCD (w & 7 equal) work on G/8 consecutive tiles, column tiles fastest,
+  // i.e. they share input row panels in their L2.  Logical tiles run over
+  // (phase, clip, row tile, column tile).
+  const int ntn = p.Cout / BN, mtiles = (p.Lq + BM - 1) / BM;
+  const int per_img = mtiles * ntn, total = per_img * p.batch * p.phases;
+  const int G = gridDim.x;
+  const int tile_base = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  int q0 = 0, co0 = 0, b = 0, ph = 0, row0 = 0;
+  const unsigned short* __restrict__ xb6 = nullptr;
+  const float* __restrict__ xbf = nullptr;
+  const unsigned short* __restrict__ wbase = nullptr;
+  auto setup = [&](int L) {
+    ph = L / (per_img * p.batch);
+    const int rem = L - ph * per_img * p.batch;
+    b = rem / per_img;
+    const int wg = rem - b * per_img;
+    const int mt = wg / ntn, nt = wg - mt * ntn;
+    q0 = mt * BM;
+    co0 = nt * BN;
+    row0 = q0 + p.in_base[ph] + lo_rel;
+    if constexpr (AF32) xbf = p.x + (long long)b * p.x_bstride;
+    else xb6 = p.x6 + (long long)b * p.x_bstride * 3;
+    wbase = p.w6 + ((long long)ph * taps * nchunks) * p.Cout * 48 + (long long)co0 * 48;
+  };
+  int L = tile_base;
+  if (L >= total) return;  // whole workgroup, before any barrier
+  setup(L);
 
   // Branch-free staging slots (surplus slots duplicate the last element).
   int a_row[A_PT], a_k[A_PT], a_lds[A_PT];
@@ -586,37 +623,45 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams 
   auto adv = [&](int& c_, int& m_) {
     if (++m_ == taps) { m_ = 0; ++c_; }
   };
-  // ---- prologue: A(0), B(0), B(1) (and A(1) when taps == 1) in LDS; the next loads in flight
-  loadA(0, ra[0]);
-  loadB(0, 0, rb[0]);
-  storeA(0, ra[0]);
-  storeB(0, rb[0]);
-  int c1 = 0, m1 = 0;  // position of step s+1
-  adv(c1, m1);
-  if (nsteps > 1) {
-    loadB(c1, m1, rb[0]);
-    storeB(1, rb[0]);
-  }
-  if (taps == 1 && nchunks > 1) {
-    loadA(1, ra[0]);
-    storeA(1, ra[0]);
-  }
-  int c2 = c1, m2 = m1;  // position of step s+2
-  adv(c2, m2);
-  int c3 = c2, m3 = m2;  // position of step s+3
-  adv(c3, m3);
-  // in flight for the first loop step: the input chunk staged next (1-tap: the one first used at
-  // step 2; with a halo: chunk 1, held in registers until step taps - 2 stores it) and B(2)
-  if constexpr (HALO > 0) {
-    if (nchunks > 1) loadA(1, ra[0]);
-  } else {
-    if (m2 == 0 && c2 < nchunks) loadA(c2, ra[1 % RA_SETS]);
-  }
-  loadB(min(c2, nchunks - 1), c2 < nchunks ? m2 : taps - 1, rb[1]);
-  __syncthreads();
-  readF(0, 0, 0, af[0], bfr[0]);
+  // step positions (chunk, tap) of s+1, s+2, s+3 and the ring slot of step s
+  int c1, m1, c2, m2, c3, m3, slot;
+  // ---- prologue, part 1 (issued before the previous tile's epilogue): A(0), B(0), B(1), and
+  //      for 1-tap convs A(1), into the staging registers
+  const int s1c = taps > 1 ? 0 : 1, s1m = taps > 1 ? 1 : 0;  // position of step 1 (nsteps >= 2)
+  auto prologue_loads = [&]() {
+    loadA(0, ra[0]);
+    if constexpr (HALO == 0) loadA(1 < nchunks ? 1 : 0, ra[1 % RA_SETS]);
+    loadB(0, 0, rb[0]);
+    loadB(s1c, s1m, rb[1]);
+  };
+  // ---- part 2: to LDS, then the loads in flight for the first loop step: the input chunk
+  //      staged next (1-tap: the one first used at step 2; with a halo: chunk 1, held in
+  //      registers until step taps - 2 stores it) and B(2)
+  auto prologue_stores = [&]() {
+    storeA(0, ra[0]);
+    if constexpr (HALO == 0) storeA(1, ra[1 % RA_SETS]);
+    storeB(0, rb[0]);
+    storeB(1, rb[1]);
+    c1 = s1c;
+    m1 = s1m;
+    c2 = c1;
+    m2 = m1;
+    adv(c2, m2);
+    c3 = c2;
+    m3 = m2;
+    adv(c3, m3);
+    slot = 0;
+    if constexpr (HALO > 0) {
+      if (nchunks > 1) loadA(1, ra[0]);
+    } else {
+      if (m2 == 0 && c2 < nchunks) loadA(c2, ra[1 % RA_SETS]);
+    }
+    loadB(min(c2, nchunks - 1), c2 < nchunks ? m2 : taps - 1, rb[1]);
+    __syncthreads();
+    readF(0, 0, 0, af[0], bfr[0]);
+  };
+  prologue_loads();
 
-  int c = 0, slot = 0;  // chunk of step s; ring slot of step s
   auto step = [&](int s, auto qtag) {
     constexpr int Q = decltype(qtag)::value;
     const int slot1 = slot == 2 ? 0 : slot + 1, slot2 = slot1 == 2 ? 0 : slot1 + 1;
@@ -659,18 +704,45 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_gemm_x6w8(const ConvParams 
     adv(c2, m2);
     adv(c3, m3);
     slot = slot1;
-    (void)c;
   };
-  // nsteps is even (launcher): without an odd exit the loop header never merges a path on which
-  // this iteration's loads are still in flight, which made the waitcnt pass emit vmcnt(0).
-  for (int s = 0; s < nsteps; s += 2) {
-    step(s, std::integral_constant<int, 0>{});
-    step(s + 1, std::integral_constant<int, 1>{});
+  for (;;) {
+    prologue_stores();
+    // nsteps is even (launcher): without an odd exit the loop header never merges a path on which
+    // this iteration's loads are still in flight, which made the waitcnt pass emit vmcnt(0).
+#ifdef DCX_CLOCK_DIAG
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    for (int s = 0; s < nsteps; s += 2) {
+      step(s, std::integral_constant<int, 0>{});
+      step(s + 1, std::integral_constant<int, 1>{});
+    }
+#ifdef DCX_CLOCK_DIAG
+    if (threadIdx.x == 0) {
+      atomicAdd(&g_clock_diag[0], __builtin_amdgcn_s_memtime() - t0);
+      atomicAdd(&g_clock_diag[1], __builtin_amdgcn_s_memrealtime() - r0);
+      atomicAdd(&g_clock_diag[2], (unsigned long long)nsteps);
+    }
+#endif
+    // the next tile's first loads go out before this tile's epilogue, which hides their latency
+    const int eq0 = q0, eco0 = co0, eb = b, eph = ph;
+    const int Ln = L + G;
+    const bool more = Ln < total;  // uniform over the workgroup
+    if (more) {
+      setup(Ln);
+      prologue_loads();
+    }
+    epilogue_lds<BM, BN, WM, WN, (2 * ABUF + 3 * BBUF) / 2, NT>(p, acc, eq0, eco0, eb, eph,
+                                                                reinterpret_cast<float*>(lds));
+    if (!more) break;
+    L = Ln;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    __syncthreads();  // the epilogue's LDS reads are done before the next prologue writes LDS
   }
-  if constexpr (ARGMIN)
-    epilogue<BM, BN, WM, WN, true>(p, acc, q0, co0, nt, ntiles, b, ph, reinterpret_cast<float*>(lds));
-  else
-    epilogue_lds<BM, BN, WM, WN, (2 * ABUF + 3 * BBUF) / 2, NT>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -853,27 +925,42 @@ static hipError_t launch_f32(const ConvParams& p, int batch, int phases, hipStre
   return hipGetLastError();
 }
 
+// Persistent launch: as many workgroups as fit on the device at once (occupancy from the
+// runtime, once per kernel), a multiple of 8 (XCD grouping), at most the tile count rounded up.
+template <int BM, int BN, int WM, int WN, int HALO, int PROD, bool AF32>
+static hipError_t launch_x6_persistent(ConvParams p, int batch, int phases, hipStream_t s) {
+  auto kern = conv_gemm_x6w8<BM, BN, WM, WN, HALO, false, PROD, AF32>;
+  static int resident = 0;  // workgroups resident per device (per instantiation)
+  if (!resident) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WM * WN, 0) != hipSuccess || per_cu < 1)
+      return hipErrorInvalidValue;
+    resident = cus * per_cu;
+  }
+  p.batch = batch;
+  p.phases = phases;
+  const long long total = (long long)((p.Lq + BM - 1) / BM) * (p.Cout / BN) * batch * phases;
+  if (total > (1LL << 30)) return hipErrorInvalidValue;
+  int g = (int)std::min<long long>(resident, (total + 7) / 8 * 8);
+  g = std::max(8, g / 8 * 8);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(64 * WM * WN), 0, s, p);
+  return hipGetLastError();
+}
+
 template <int BM, int BN, int WM, int WN, int HALO, bool ARGMIN>
 static hipError_t launch_x6w8(const ConvParams& p, int batch, int phases, hipStream_t s) {
-  const int mtiles = (p.Lq + BM - 1) / BM;
-  dim3 grid(mtiles * (p.Cout / BN), batch, phases);
-  if (p.nprod == 1)
-    hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, WM, WN, HALO, ARGMIN, 1>), grid, dim3(64 * WM * WN), 0, s, p);
-  else
-    hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, WM, WN, HALO, ARGMIN, 6>), grid, dim3(64 * WM * WN), 0, s, p);
-  return hipGetLastError();
+  static_assert(!ARGMIN, "x6 VQ search uses vq_prefilter_x3");
+  return p.nprod == 1 ? launch_x6_persistent<BM, BN, WM, WN, HALO, 1, false>(p, batch, phases, s)
+                      : launch_x6_persistent<BM, BN, WM, WN, HALO, 6, false>(p, batch, phases, s);
 }
 
 // fp32-input variant (Cin <= 64 convs, see conv_gemm_x6w8)
 template <int BM, int BN, int WM, int WN, int HALO>
 static hipError_t launch_x6w8_af32(const ConvParams& p, int batch, int phases, hipStream_t s) {
-  const int mtiles = (p.Lq + BM - 1) / BM;
-  dim3 grid(mtiles * (p.Cout / BN), batch, phases);
-  if (p.nprod == 1)
-    hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, WM, WN, HALO, false, 1, true>), grid, dim3(64 * WM * WN), 0, s, p);
-  else
-    hipLaunchKernelGGL((conv_gemm_x6w8<BM, BN, WM, WN, HALO, false, 6, true>), grid, dim3(64 * WM * WN), 0, s, p);
-  return hipGetLastError();
+  return p.nprod == 1 ? launch_x6_persistent<BM, BN, WM, WN, HALO, 1, true>(p, batch, phases, s)
+                      : launch_x6_persistent<BM, BN, WM, WN, HALO, 6, true>(p, batch, phases, s);
 }
 
 static int tap_span(const ConvParams& p) { return (p.taps - 1) * (p.in_step < 0 ? -p.in_step : p.in_step); }
@@ -890,7 +977,7 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       if (kname) *kname = b1 ? bf : x6;
     };
     if (!p.x6) {  // fp32 input, split while staging: small-Cout tiles only
-      if (!p.x || p.Cin > 64 || p.Cout > 64 || p.taps < 2) return hipErrorInvalidValue;
+      if (!p.x || p.Cin > 128 || p.Cout > 64 || p.taps < 2) return hipErrorInvalidValue;
       if (p.Cout == 64) {
         name("conv_gemm_x6w4f<256,64,halo>", "conv_gemm_bf16w4f<256,64,halo>");
         return launch_x6w8_af32<256, 64, 4, 1, 64>(p, batch, phases, s);

@@ -54,6 +54,8 @@ struct ConvParams {
   // planes-mode arithmetic: 6 = x6 (fp32-accurate), 1 = bf16 (hi plane only, one product);
   // round_bf16: round the GEMM result (after bias, and after GELU) to bf16 like torch.autocast
   int nprod, round_bf16;
+  // persistent x6 kernels: tiles are enumerated over (phase, clip, row tile, column tile)
+  int batch, phases;
 };
 
 // Launchers (all stream-ordered, no allocation).  Return hipError_t of the launch.
