@@ -746,6 +746,219 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) conv_gemm_x6w8(const ConvPara
 }
 
 // ---------------------------------------------------------------------------------------------
+// Ping-pong x6 conv kernel for the dominant shape (256 x 128 tile, tap halo, planes input).
+//
+// The two waves on each SIMD (wave w and w + 4) belong to different groups: group 0 = waves 0-3
+// (tile rows 0-127), group 1 = waves 4-7 (rows 128-255).  Segments are separated by barriers that
+// all 8 waves execute; group 0 runs  MFMA(s) | MEM0(s)  and group 1 runs  MEM1(s) | MFMA(s),  so
+// in every segment one wave per SIMD issues its 24 MFMAs while its partner reads fragments,
+// stores staged tiles and issues global loads, and the matrix pipe no longer idles while both
+// waves of a SIMD do their memory work at the same time (conv_gemm_x6w8: ~1/3 of each step).
+//
+// Segment k = 2s: group 0 MFMA(s), group 1 MEM1(s);  k = 2s+1: group 0 MEM0(s), group 1 MFMA(s).
+//   MEM0(s): fragments of step s+1; store its half of step s+2; load its half of step s+3.
+//   MEM1(s): fragments of step s;   store its half of step s+1; load its half of step s+2.
+// Step t's data is complete after segment 2t-2 and is read in segments 2t-1 (group 0) and 2t
+// (group 1), so the weight ring needs only 2 slots (t & 1): step t+2 is written in segments 2t+1
+// and 2t+2.  Input tiles are double-buffered by chunk parity and follow the schedule of their
+// chunk's first step.  Each group stages half of every tile (both halves with the same maps).
+// ---------------------------------------------------------------------------------------------
+template <int HALO>
+__global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
+  constexpr int BM = 256, BN = 128, WN = 2;
+  constexpr int WR = 64, WC = 64, TM = 2, TN = 2;
+  constexpr int XROW = 56;  // padded 112-byte rows
+  constexpr int AROWS = BM + HALO;
+  constexpr int A_P = AROWS * 6, B_P = BN * 6;          // 16-byte pieces per tile
+  constexpr int A_H = A_P / 2, B_H = B_P / 2;           // per group
+  constexpr int A_PT = (A_H + 255) / 256, B_PT = (B_H + 255) / 256;
+  constexpr int ABUF = AROWS * XROW, BBUF = BN * XROW;
+  static_assert(A_P % 2 == 0 && B_P % 2 == 0, "halves");
+  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * ABUF + 2 * BBUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int group = __builtin_amdgcn_readfirstlane(tid >> 8), gt = tid & 255;
+  const int wm = wave / WN, wn = wave % WN;
+  const int ntiles = p.Cout / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = wg / ntiles, nt = wg - mt * ntiles;
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int b = blockIdx.y, ph = blockIdx.z;
+  const unsigned short* __restrict__ xb6 = p.x6 + (long long)b * p.x_bstride * 3;
+  const long long ldx6 = (long long)p.ldx * 3;
+  const int nchunks = p.Cin / BK;
+  const int taps = p.taps;
+  const int nsteps = nchunks * taps;
+  const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
+  const int row0 = q0 + p.in_base[ph] + lo_rel;
+  const unsigned short* __restrict__ wbase =
+      p.w6 + ((long long)ph * taps * nchunks) * p.Cout * 48 + (long long)co0 * 48;
+  const long long wslab = (long long)p.Cout * 48;
+  const int lin = p.Lin;
+
+  // this thread's staging slots in its group's half of each tile (surplus slots repeat the last)
+  int a_row[A_PT], a_k[A_PT], b_off[B_PT], b_lds[B_PT];
+#pragma unroll
+  for (int i = 0; i < A_PT; ++i) {
+    const int idx = group * A_H + min(gt + 256 * i, A_H - 1);
+    a_row[i] = idx / 6;
+    a_k[i] = idx - a_row[i] * 6;
+  }
+#pragma unroll
+  for (int i = 0; i < B_PT; ++i) {
+    const int idx = group * B_H + min(gt + 256 * i, B_H - 1);
+    const int col = idx / 6, piece = idx - col * 6;
+    b_off[i] = idx * 8;
+    b_lds[i] = col * XROW + piece * 8;
+  }
+  f32x4 ra[A_PT], rb[B_PT];
+  auto loadA = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) {
+      const int ir = row0 + a_row[i];
+      const bool ok = ir >= 0 && ir < lin;
+      const unsigned short* src =
+          ok ? xb6 + (long long)ir * ldx6 + c * 48 + a_k[i] * 8 : reinterpret_cast<const unsigned short*>(g_zero_row);
+      ra[i] = *reinterpret_cast<const f32x4*>(src);
+    }
+  };
+  auto storeA = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i)
+      *reinterpret_cast<f32x4*>(lds + buf * ABUF + a_row[i] * XROW + a_k[i] * 8) = ra[i];
+  };
+  auto loadB = [&](int c, int m) {
+    const unsigned short* src = wbase + ((long long)m * nchunks + c) * wslab;
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) rb[i] = *reinterpret_cast<const f32x4*>(src + b_off[i]);
+  };
+  auto storeB = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) *reinterpret_cast<f32x4*>(lds + 2 * ABUF + slot * BBUF + b_lds[i]) = rb[i];
+  };
+
+  const int lrow = lane & 31, hoff = (lane >> 5) * 24;
+  s16x8 af[TM][3], bfr[TN][3];
+  auto readF = [&](int c, int m, int slot) {
+    const int off = m * p.in_step - lo_rel;
+    const unsigned short* A = lds + (c & 1) * ABUF;
+    const unsigned short* Bsm = lds + 2 * ABUF + slot * BBUF;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const unsigned short* ap = A + (wm * WR + i * 32 + lrow + off) * XROW + hoff;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) af[i][pl] = *reinterpret_cast<const s16x8*>(ap + pl * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const unsigned short* bp = Bsm + (wn * WC + j * 32 + lrow) * XROW + hoff;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = *reinterpret_cast<const s16x8*>(bp + pl * 8);
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // s_setprio around the cluster keeps hipcc from moving MFMAs across the segment barriers
+  // (cdna_hip_programming.md T5), which would collapse the ping-pong
+  auto mfma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#define DCX_MF(i, j, x, y) \
+  acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[i][x]), \
+                                                      __builtin_bit_cast(bf16x8, bfr[j][y]), acc[i][j], 0, 0, 0)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        DCX_MF(i, j, 2, 0);
+        DCX_MF(i, j, 1, 1);
+        DCX_MF(i, j, 0, 2);
+        DCX_MF(i, j, 1, 0);
+        DCX_MF(i, j, 0, 1);
+        DCX_MF(i, j, 0, 0);
+      }
+#undef DCX_MF
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto adv = [&](int& c_, int& m_) {
+    if (++m_ == taps) { m_ = 0; ++c_; }
+  };
+
+  // ---- prologue: both groups stage their halves of A(0), B(0), B(1); A(1) when step 1 opens it
+  loadA(0);
+  loadB(0, 0);
+  storeA(0);
+  storeB(0);
+  int c1 = 0, m1 = 0;  // position of step 1
+  adv(c1, m1);
+  loadB(c1, m1);
+  storeB(1);
+  if (m1 == 0) {  // taps == 1
+    loadA(1);
+    storeA(1);
+  }
+  // position of the step this group stores next (group 0: step 2 in MEM0(0); group 1: step 2 in
+  // MEM1(1)) and of the step it reads next; both groups start their loads for step 2
+  int cw = c1, mw = m1;
+  adv(cw, mw);                        // step 2
+  int cl = cw, ml = mw;               // next load: step 2
+  if (nsteps > 2) {
+    loadB(cl, ml);
+    if (ml == 0) loadA(cl);
+  }
+  adv(cl, ml);                        // step 3
+  __syncthreads();
+  int cr = 0, mr = 0;                 // position of the step whose fragments are read next
+  if (group == 0) {
+    readF(0, 0, 0);
+    adv(cr, mr);                      // group 0 reads step 1 in MEM0(0)
+    for (int s = 0; s < nsteps; ++s) {
+      mfma();                         // MFMA(s)
+      __syncthreads();
+      // MEM0(s): fragments of step s+1, store step s+2, load step s+3
+      if (s + 1 < nsteps) readF(cr, mr, (s + 1) & 1);
+      if (s + 2 < nsteps) {
+        storeB((s + 2) & 1);
+        if (mw == 0) storeA(cw & 1);
+      }
+      if (s + 3 < nsteps) {
+        loadB(cl, ml);
+        if (ml == 0) loadA(cl);
+      }
+      adv(cr, mr);
+      adv(cw, mw);
+      adv(cl, ml);
+      __syncthreads();
+    }
+  } else {
+    for (int s = 0; s < nsteps; ++s) {
+      // MEM1(s): fragments of step s, store step s+1 (steps 0, 1 came from the prologue),
+      // load step s+2 (step 2 was loaded in the prologue)
+      readF(cr, mr, s & 1);
+      if (s >= 1 && s + 1 < nsteps) {
+        storeB((s + 1) & 1);
+        if (mw == 0) storeA(cw & 1);
+        adv(cw, mw);
+      }
+      if (s >= 1 && s + 2 < nsteps) {
+        loadB(cl, ml);
+        if (ml == 0) loadA(cl);
+        adv(cl, ml);
+      }
+      adv(cr, mr);
+      __syncthreads();
+      mfma();                         // MFMA(s)
+      __syncthreads();
+    }
+  }
+  epilogue_lds<BM, BN, 4, WN, (2 * ABUF + 2 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+}
+
+// ---------------------------------------------------------------------------------------------
 // VQ prefilter GEMM (x6 mode): approximate x.e from hi*hi + hi*mid + mid*hi of the planes
 // (bound in launch_vq_prefilter), per-tile top 2 of (x2 + e2) - 2 x.e (epilogue_top2).
 //
@@ -990,6 +1203,14 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       return launch_x6w8<128, 128, 2, 2, 0, false>(p, batch, phases, s);
     }
     if (p.Cout % 128 == 0) {
+#ifndef DCX_NO_PP
+      if (!b1) {  // x6: ping-pong kernel
+        if (kname) *kname = "conv_gemm_x6pp<256,128,halo>";
+        const int mtiles = (p.Lq + 255) / 256;
+        hipLaunchKernelGGL((conv_gemm_x6pp<64>), dim3(mtiles * (p.Cout / 128), batch, phases), dim3(512), 0, s, p);
+        return hipGetLastError();
+      }
+#endif
       name("conv_gemm_x6w8<256,128,halo>", "conv_gemm_bf16w8<256,128,halo>");
       return launch_x6w8<256, 128, 4, 2, 64, false>(p, batch, phases, s);
     }
