@@ -912,6 +912,9 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
   }
   adv(cl, ml);                        // step 3
   __syncthreads();
+#ifdef DCX_CLOCK_DIAG
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   int cr = 0, mr = 0;                 // position of the step whose fragments are read next
   if (group == 0) {
     readF(0, 0, 0);
@@ -955,6 +958,13 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
       __syncthreads();
     }
   }
+#ifdef DCX_CLOCK_DIAG
+  if (threadIdx.x == 0) {
+    atomicAdd(&g_clock_diag[0], __builtin_amdgcn_s_memtime() - t0);
+    atomicAdd(&g_clock_diag[1], __builtin_amdgcn_s_memrealtime() - r0);
+    atomicAdd(&g_clock_diag[2], (unsigned long long)nsteps);
+  }
+#endif
   epilogue_lds<BM, BN, 4, WN, (2 * ABUF + 2 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
@@ -1198,6 +1208,14 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       name("conv_gemm_x6w4f<256,32,halo>", "conv_gemm_bf16w4f<256,32,halo>");
       return launch_x6w8_af32<256, 32, 4, 1, 64>(p, batch, phases, s);
     }
+#ifndef DCX_NO_PP
+    if (p.Cout % 128 == 0 && !h && !b1) {  // x6 1-tap: ping-pong kernel without halo
+      if (kname) *kname = "conv_gemm_x6pp<256,128>";
+      const int mtiles = (p.Lq + 255) / 256;
+      hipLaunchKernelGGL((conv_gemm_x6pp<0>), dim3(mtiles * (p.Cout / 128), batch, phases), dim3(512), 0, s, p);
+      return hipGetLastError();
+    }
+#endif
     if (p.Cout % 128 == 0 && !h) {  // 1-tap: 4-wave 128 x 128 tiles, two workgroups per CU
       name("conv_gemm_x6w4<128,128>", "conv_gemm_bf16w4<128,128>");
       return launch_x6w8<128, 128, 2, 2, 0, false>(p, batch, phases, s);
