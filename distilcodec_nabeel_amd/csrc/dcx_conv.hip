@@ -763,10 +763,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) conv_gemm_x6w8(const ConvPara
 // and 2t+2.  Input tiles are double-buffered by chunk parity and follow the schedule of their
 // chunk's first step.  Each group stages half of every tile (both halves with the same maps).
 // ---------------------------------------------------------------------------------------------
-template <int HALO>
+template <int HALO, int BN>
 __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
-  constexpr int BM = 256, BN = 128, WN = 2;
-  constexpr int WR = 64, WC = 64, TM = 2, TN = 2;
+  // wave tiles 64 x (BN / 2): 24 MFMAs per segment at BN = 128
+  static_assert(BN == 128 || BN == 256, "column tile");
+  constexpr int BM = 256, WN = 2;
+  constexpr int WR = 64, WC = BN / WN, TM = 2, TN = WC / 32;
   constexpr int XROW = 56;  // padded 112-byte rows
   constexpr int AROWS = BM + HALO;
   constexpr int A_P = AROWS * 6, B_P = BN * 6;          // 16-byte pieces per tile
@@ -966,6 +968,15 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
   }
 #endif
   epilogue_lds<BM, BN, 4, WN, (2 * ABUF + 2 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+}
+
+template <int HALO>
+static hipError_t launch_x6pp(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
+  // (BN = 256 needs 128 accumulator + 72 fragment VGPRs and spills at 2 waves per SIMD)
+  const int mtiles = (p.Lq + 255) / 256;
+  if (kname) *kname = HALO ? "conv_gemm_x6pp<256,128,halo>" : "conv_gemm_x6pp<256,128>";
+  hipLaunchKernelGGL((conv_gemm_x6pp<HALO, 128>), dim3(mtiles * (p.Cout / 128), batch, phases), dim3(512), 0, s, p);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1209,12 +1220,7 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       return launch_x6w8_af32<256, 32, 4, 1, 64>(p, batch, phases, s);
     }
 #ifndef DCX_NO_PP
-    if (p.Cout % 128 == 0 && !h && !b1) {  // x6 1-tap: ping-pong kernel without halo
-      if (kname) *kname = "conv_gemm_x6pp<256,128>";
-      const int mtiles = (p.Lq + 255) / 256;
-      hipLaunchKernelGGL((conv_gemm_x6pp<0>), dim3(mtiles * (p.Cout / 128), batch, phases), dim3(512), 0, s, p);
-      return hipGetLastError();
-    }
+    if (p.Cout % 128 == 0 && !h && !b1) return launch_x6pp<0>(p, batch, phases, s, kname);  // x6 1-tap
 #endif
     if (p.Cout % 128 == 0 && !h) {  // 1-tap: 4-wave 128 x 128 tiles, two workgroups per CU
       name("conv_gemm_x6w4<128,128>", "conv_gemm_bf16w4<128,128>");
@@ -1222,12 +1228,7 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
     }
     if (p.Cout % 128 == 0) {
 #ifndef DCX_NO_PP
-      if (!b1) {  // x6: ping-pong kernel
-        if (kname) *kname = "conv_gemm_x6pp<256,128,halo>";
-        const int mtiles = (p.Lq + 255) / 256;
-        hipLaunchKernelGGL((conv_gemm_x6pp<64>), dim3(mtiles * (p.Cout / 128), batch, phases), dim3(512), 0, s, p);
-        return hipGetLastError();
-      }
+      if (!b1) return launch_x6pp<64>(p, batch, phases, s, kname);  // x6: ping-pong kernel
 #endif
       name("conv_gemm_x6w8<256,128,halo>", "conv_gemm_bf16w8<256,128,halo>");
       return launch_x6w8<256, 128, 4, 2, 64, false>(p, batch, phases, s);
