@@ -29,10 +29,12 @@ def short(name):
     if base == "vq_prefilter_x3":
         kind = "vq_prefilter_x3" if len(parts) < 5 or parts[4] == "true" else "vq_prefilter_x2"
         return f"{kind}<{parts[0]},{parts[1]}>"
-    if base == "conv_gemm_x6w8":  # <BM, BN, WM, WN, HALO, ARGMIN>: bench.py's profile names
+    if base == "conv_gemm_x6w8":  # <BM, BN, WM, WN, HALO, ARGMIN, PROD, AF32>: bench.py's names
         waves = int(parts[2]) * int(parts[3])
         halo = ",halo" if parts[4] != "0" else ""
-        return f"conv_gemm_x6w{waves}<{parts[0]},{parts[1]}{halo}>"
+        kind = "bf16" if len(parts) > 6 and parts[6] == "1" else "x6"
+        f = "f" if len(parts) > 7 and parts[7] == "true" else ""
+        return f"conv_gemm_{kind}w{waves}{f}<{parts[0]},{parts[1]}{halo}>"
     return base + targs.replace(" ", "")
 
 
