@@ -503,6 +503,7 @@ struct ConvCall {
   const float* gamma = nullptr;
   int epi = dcx::EPI_BIAS, mean = dcx::MEAN_NONE;
   bool exact = false;  // keep x6 arithmetic in bf16 mode (the reference's fp32 mel front end)
+  bool silu_in = false;  // fp32 input: the conv consumes silu(x) (applied while staging)
   void silu_to(const Act& a) { y2 = a.f; y6s = a.p; }
   void out_to(const Act& a) { y = a.f; y6 = a.p; }
 };
@@ -514,6 +515,7 @@ bool f32_input_ok(const ConvW& w) { return w.cin <= 128 && w.cout <= 64 && w.tap
 int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, bool force_f32 = false) {
   const bool x6 = x6_mode(h) && !force_f32;
   const bool x6_f32in = x6 && !c.x.p && c.x.f && f32_input_ok(w);
+  if (c.silu_in && !x6_f32in) return fail(h, DCX_ERR_STATE, "internal: silu_in needs an fp32-input conv");
   if (x6 ? ((!c.x.p && !x6_f32in) || !w.w6) : !c.x.f)
     return fail(h, DCX_ERR_STATE, "internal: conv input missing for GEMM mode");
   ConvParams p{};
@@ -547,6 +549,7 @@ int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, boo
   const bool one = x6 && h->gemm_mode == DCX_GEMM_BF16 && !c.exact;
   p.nprod = one ? 1 : 6;
   p.round_bf16 = one;
+  p.silu_in = c.silu_in;
   ProfScope ps(h, s);
   const char* kname = "conv";
   HIPCHK(h, dcx::launch_conv(p, c.batch, w.phases, s, &kname));
@@ -806,19 +809,23 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
     const int Co = up.cout, Lo = L * c.up_rates[i];
     const ConvW& rconv = h->res[i][0][0][0];  // every ResBlock conv of the stage has Cin = Cout = Co
     const Act S_i = in_form(S, up), XS_i = in_form(XS, rconv), RS_i = in_form(RS, rconv), Tb_i = in_form(Tb, rconv);
+    // fp32-input stages: the first conv of each pair applies silu to X / R while staging, so
+    // silu(X) and silu(R) are never written (7 activation tensors per stage less HBM traffic)
+    const bool silu_on_load = x6_mode(h) && f32_input_ok(rconv);
     {
       ConvCall cc = framed(S_i, B, L, C);
       cc.y = X;
-      cc.silu_to(XS_i);
+      if (!silu_on_load) cc.silu_to(XS_i);
       RUN(run_conv(h, up, cc, s));
     }
     const bool last_stage = i == c.n_ups - 1;
     for (int rb = 0; rb < c.n_res; ++rb) {
       for (int ci = 0; ci < 3; ++ci) {
-        const Act& src = ci == 0 ? XS_i : RS_i;
+        const Act& src = silu_on_load ? Act{ci == 0 ? X : R, nullptr} : (ci == 0 ? XS_i : RS_i);
         const float* resid = ci == 0 ? X : R;
         {
           ConvCall cc = framed(src, B, Lo, Co);
+          cc.silu_in = silu_on_load;
           cc.silu_to(Tb_i);
           RUN(run_conv(h, h->res[i][rb][ci][0], cc, s));
         }
@@ -827,7 +834,7 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
         cc.res = resid;
         if (ci < 2) {
           cc.y = R;
-          cc.silu_to(RS_i);
+          if (!silu_on_load) cc.silu_to(RS_i);
         } else {
           cc.macc = Mx;
           cc.mean = rb == 0 ? dcx::MEAN_FIRST : (rb == c.n_res - 1 ? dcx::MEAN_LAST : dcx::MEAN_MID);

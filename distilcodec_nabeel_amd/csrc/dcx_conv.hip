@@ -557,7 +557,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) conv_gemm_x6w8(const ConvPara
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           unsigned short hb, mb, lb;
-          split3(r[i][e], hb, mb, lb);
+          split3(p.silu_in ? silu_f(r[i][e]) : r[i][e], hb, mb, lb);  // silu(0) = 0: padding stays 0
           hv[e] = (short)hb;
           mv[e] = (short)mb;
           lv[e] = (short)lb;

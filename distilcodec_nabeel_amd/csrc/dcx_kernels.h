@@ -56,6 +56,9 @@ struct ConvParams {
   int nprod, round_bf16;
   // persistent x6 kernels: tiles are enumerated over (phase, clip, row tile, column tile)
   int batch, phases;
+  // fp32-input (AF32) kernels: apply silu to the input while staging (the producer then writes
+  // only the fp32 tensor, not its silu as well)
+  int silu_in;
 };
 
 // Launchers (all stream-ordered, no allocation).  Return hipError_t of the launch.
