@@ -91,6 +91,23 @@ extern "C" int dcx_diag_clock(unsigned long long* out3, int reset) {
   return 0;
 }
 #endif
+#ifdef DCX_SEG_DIAG
+// Diagnostic build only: per-segment shader-clock sums of conv_gemm_x6pp's main loop, for wave 0
+// (group 0, [0..5]) and wave 4 (group 1, [6..11]): MFMA issue, barrier wait, fragment-read issue,
+// stores (with their vmcnt wait), loads + loop control, barrier wait; [12] steps.
+__device__ unsigned long long g_seg_diag[13];
+extern "C" int dcx_diag_seg(unsigned long long* out13, int reset) {
+  if (hipMemcpyFromSymbol(out13, HIP_SYMBOL(g_seg_diag), sizeof(unsigned long long) * 13) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned long long z[13] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_seg_diag), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#define DCX_SEGT(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define DCX_SEGT(v)
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // Conv epilogue through LDS: the accumulator tile is written to LDS (in row passes that fit the
@@ -114,6 +131,10 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, f32x16 (&acc)[
   const long long ob = (long long)b * p.y_bstride;
   unsigned short* y6 = p.y6 ? p.y6 + ob * 3 : nullptr;
   unsigned short* y6s = p.y6s ? p.y6s + ob * 3 : nullptr;
+  static_assert(NT % (BN / 4) == 0, "each thread keeps one 4-channel group");
+  const int c4 = (tid % (BN / 4)) * 4, trow = tid / (BN / 4), co = co0 + c4;
+  const f32x4 bias4 = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 gamma4 = p.epi == EPI_GAMMA_RES ? *reinterpret_cast<const f32x4*>(p.gamma + co) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
   for (int r0 = 0; r0 < BM; r0 += RPP) {
     __syncthreads();
@@ -129,50 +150,66 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, f32x16 (&acc)[
           }
     }
     __syncthreads();
+    // Each thread always finishes the same 4 output channels (NT is a multiple of BN / 4), so
+    // bias and gamma are loaded once per tile, and the residual / mean-accumulator loads of IB
+    // rows are issued before their stores: the stores may alias them (the in-place ResBlock
+    // state), so hipcc would otherwise wait for one memory round trip per row.
+    constexpr int RSTEP = NT / (BN / 4), ROWS_T = RPP / RSTEP, IB = ROWS_T < 4 ? ROWS_T : 4;
+    static_assert(RPP % RSTEP == 0 && ROWS_T % IB == 0, "epilogue rows per thread");
 #pragma unroll 1
-    for (int idx = tid; idx < RPP * (BN / 4); idx += NT) {
-      const int rl = idx / (BN / 4), c4 = (idx - rl * (BN / 4)) * 4;
-      const int q = q0 + r0 + rl;
-      if (q >= p.Lq) continue;
-      const int co = co0 + c4;
-      const long long orow = (long long)q * p.out_mul + ph;
-      const long long o = ob + orow * p.ldy + co;
-      f32x4 v = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + c4);
-      if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + co);
-      if (p.round_bf16) v = round_bf16x4(v);
-      switch (p.epi) {
-        case EPI_GELU:
+    for (int rb = 0; rb < ROWS_T; rb += IB) {
+      f32x4 v[IB], r[IB], m[IB];
+      long long o[IB], orow[IB];
+      bool ok[IB];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
-          if (p.round_bf16) v = round_bf16x4(v);
-          break;
-        case EPI_GAMMA_RES:
-          v = *reinterpret_cast<const f32x4*>(p.res + o) + *reinterpret_cast<const f32x4*>(p.gamma + co) * v;
-          break;
-        case EPI_RES: v = *reinterpret_cast<const f32x4*>(p.res + o) + v; break;
-        case EPI_LOGCLAMP:
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = logf(fmaxf(v[e], 1e-5f));
-          break;
-        default: break;
+      for (int k = 0; k < IB; ++k) {
+        const int rl = trow + (rb + k) * RSTEP;
+        const int q = q0 + r0 + rl;
+        ok[k] = q < p.Lq;
+        orow[k] = (long long)q * p.out_mul + ph;
+        o[k] = ob + orow[k] * p.ldy + co;
+        v[k] = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + c4);
+        if (ok[k] && (p.epi == EPI_GAMMA_RES || p.epi == EPI_RES)) r[k] = *reinterpret_cast<const f32x4*>(p.res + o[k]);
+        if (ok[k] && (p.mean_mode == MEAN_MID || p.mean_mode == MEAN_LAST))
+          m[k] = *reinterpret_cast<const f32x4*>(p.macc + o[k]);
       }
-      if (p.mean_mode == MEAN_FIRST) {
-        *reinterpret_cast<f32x4*>(p.macc + o) = v;
-        continue;
-      } else if (p.mean_mode == MEAN_MID) {
-        *reinterpret_cast<f32x4*>(p.macc + o) = *reinterpret_cast<const f32x4*>(p.macc + o) + v;
-        continue;
-      } else if (p.mean_mode == MEAN_LAST) {
-        v = (*reinterpret_cast<const f32x4*>(p.macc + o) + v) / 3.0f;
-      }
-      if (p.y) *reinterpret_cast<f32x4*>(p.y + o) = v;
-      if (y6) store_planes4(y6, orow, p.Cout, co, v[0], v[1], v[2], v[3]);
-      if (p.y2 || y6s) {
-        f32x4 sv;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) sv[e] = silu_f(v[e]);
-        if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
-        if (y6s) store_planes4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+      for (int k = 0; k < IB; ++k) {
+        if (!ok[k]) continue;
+        f32x4 x = v[k] + bias4;
+        if (p.round_bf16) x = round_bf16x4(x);
+        switch (p.epi) {
+          case EPI_GELU:
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] = gelu_f(x[e]);
+            if (p.round_bf16) x = round_bf16x4(x);
+            break;
+          case EPI_GAMMA_RES: x = r[k] + gamma4 * x; break;
+          case EPI_RES: x = r[k] + x; break;
+          case EPI_LOGCLAMP:
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] = logf(fmaxf(x[e], 1e-5f));
+            break;
+          default: break;
+        }
+        if (p.mean_mode == MEAN_FIRST) {
+          *reinterpret_cast<f32x4*>(p.macc + o[k]) = x;
+          continue;
+        } else if (p.mean_mode == MEAN_MID) {
+          *reinterpret_cast<f32x4*>(p.macc + o[k]) = m[k] + x;
+          continue;
+        } else if (p.mean_mode == MEAN_LAST) {
+          x = (m[k] + x) / 3.0f;
+        }
+        if (p.y) *reinterpret_cast<f32x4*>(p.y + o[k]) = x;
+        if (y6) store_planes4(y6, orow[k], p.Cout, co, x[0], x[1], x[2], x[3]);
+        if (p.y2 || y6s) {
+          f32x4 sv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sv[e] = silu_f(x[e]);
+          if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o[k]) = sv;
+          if (y6s) store_planes4(y6s, orow[k], p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+        }
       }
     }
   }
@@ -918,18 +955,30 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
   const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
   int cr = 0, mr = 0;                 // position of the step whose fragments are read next
+#ifdef DCX_SEG_DIAG
+  unsigned long long sd[6] = {}, tprev = 0;
+#endif
   if (group == 0) {
     readF(0, 0, 0);
     adv(cr, mr);                      // group 0 reads step 1 in MEM0(0)
     for (int s = 0; s < nsteps; ++s) {
+      DCX_SEGT(ta);
+#ifdef DCX_SEG_DIAG
+      if (s) sd[5] += ta - tprev;
+#endif
       mfma();                         // MFMA(s)
+      DCX_SEGT(tb);
       __syncthreads();
-      // MEM0(s): fragments of step s+1, store step s+2, load step s+3
+      DCX_SEGT(tc);
+      // MEM0(s): fragments of step s+1, store step s+2, load step s+3 (issuing the loads before
+      // the fragment reads was slower: 2480 vs 2048 cycles per step at k11)
       if (s + 1 < nsteps) readF(cr, mr, (s + 1) & 1);
+      DCX_SEGT(tc1);
       if (s + 2 < nsteps) {
         storeB((s + 2) & 1);
         if (mw == 0) storeA(cw & 1);
       }
+      DCX_SEGT(tc2);
       if (s + 3 < nsteps) {
         loadB(cl, ml);
         if (ml == 0) loadA(cl);
@@ -937,27 +986,312 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
       adv(cr, mr);
       adv(cw, mw);
       adv(cl, ml);
+      DCX_SEGT(td);
       __syncthreads();
+#ifdef DCX_SEG_DIAG
+      sd[0] += tb - ta;
+      sd[1] += tc - tb;
+      sd[2] += tc1 - tc;
+      sd[3] += tc2 - tc1;
+      sd[4] += td - tc2;
+      tprev = td;
+#endif
     }
   } else {
     for (int s = 0; s < nsteps; ++s) {
       // MEM1(s): fragments of step s, store step s+1 (steps 0, 1 came from the prologue),
       // load step s+2 (step 2 was loaded in the prologue)
+      DCX_SEGT(ta);
+#ifdef DCX_SEG_DIAG
+      if (s) sd[1] += ta - tprev;
+#endif
       readF(cr, mr, s & 1);
+      DCX_SEGT(ta1);
       if (s >= 1 && s + 1 < nsteps) {
         storeB((s + 1) & 1);
         if (mw == 0) storeA(cw & 1);
         adv(cw, mw);
       }
+      DCX_SEGT(ta2);
       if (s >= 1 && s + 2 < nsteps) {
         loadB(cl, ml);
         if (ml == 0) loadA(cl);
         adv(cl, ml);
       }
       adv(cr, mr);
+      DCX_SEGT(tb);
       __syncthreads();
+      DCX_SEGT(tc);
       mfma();                         // MFMA(s)
+      DCX_SEGT(td);
       __syncthreads();
+#ifdef DCX_SEG_DIAG
+      sd[2] += ta1 - ta;
+      sd[3] += ta2 - ta1;
+      sd[4] += tb - ta2;
+      sd[5] += tc - tb;
+      sd[0] += td - tc;
+      tprev = td;
+#endif
+    }
+  }
+#ifdef DCX_SEG_DIAG
+  if ((threadIdx.x & 255) == 0) {
+    const int o = group * 6;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) atomicAdd(&g_seg_diag[o + i], sd[i]);
+    if (group == 0) atomicAdd(&g_seg_diag[12], (unsigned long long)nsteps);
+  }
+#endif
+#ifdef DCX_CLOCK_DIAG
+  if (threadIdx.x == 0) {
+    atomicAdd(&g_clock_diag[0], __builtin_amdgcn_s_memtime() - t0);
+    atomicAdd(&g_clock_diag[1], __builtin_amdgcn_s_memrealtime() - r0);
+    atomicAdd(&g_clock_diag[2], (unsigned long long)nsteps);
+  }
+#endif
+  epilogue_lds<BM, BN, 4, WN, (2 * ABUF + 2 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+}
+
+// ---------------------------------------------------------------------------------------------
+// conv_gemm_x6lm: conv_gemm_x6pp with the global loads moved into the MFMA segments.
+//
+// Per-segment stamps of conv_gemm_x6pp (tools/seg_diag.py) show its MEM segment, not the MFMA
+// segment, setting the pace: at k11 a wave spends ~310 cycles issuing its 12 fragment reads,
+// ~180 on its LDS stores and ~570 issuing 2-6 global loads behind them, against ~800 for 24
+// MFMAs, so the MFMA wave then waits ~250-450 cycles at the barrier.  Here each wave issues its
+// next loads at the head of its MFMA segment, while its SIMD partner is the one using LDS, into
+// a second staging register set: step t is loaded in MFMA(t - 3) into set t & 1 and stored by
+// group 0 in MEM0(t - 2), by group 1 in MEM1(t - 1) (three segments of latency cover either way).
+// The loop is unrolled by two so the register sets are static.  Input-chunk loads (conditional)
+// go before the weight loads (unconditional, index clamped at the tail), so the weight loads are
+// always the youngest and the stores' vmcnt waits stay counted.
+// ---------------------------------------------------------------------------------------------
+template <int HALO>
+__global__ void __launch_bounds__(512, 2) conv_gemm_x6lm(const ConvParams p) {
+  constexpr int BM = 256, BN = 128, WN = 2;
+  constexpr int WR = 64, WC = BN / WN, TM = 2, TN = WC / 32;
+  constexpr int XROW = 56;  // padded 112-byte rows
+  constexpr int AROWS = BM + HALO;
+  constexpr int A_P = AROWS * 6, B_P = BN * 6;
+  constexpr int A_H = A_P / 2, B_H = B_P / 2;
+  constexpr int A_PT = (A_H + 255) / 256, B_PT = (B_H + 255) / 256;
+  constexpr int ABUF = AROWS * XROW, BBUF = BN * XROW;
+  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * ABUF + 2 * BBUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int group = __builtin_amdgcn_readfirstlane(tid >> 8), gt = tid & 255;
+  const int wm = wave / WN, wn = wave % WN;
+  const int ntiles = p.Cout / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = wg / ntiles, nt = wg - mt * ntiles;
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int b = blockIdx.y, ph = blockIdx.z;
+  const unsigned short* __restrict__ xb6 = p.x6 + (long long)b * p.x_bstride * 3;
+  const long long ldx6 = (long long)p.ldx * 3;
+  const int nchunks = p.Cin / BK;
+  const int taps = p.taps;
+  const int nsteps = nchunks * taps;
+  const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
+  const int row0 = q0 + p.in_base[ph] + lo_rel;
+  const unsigned short* __restrict__ wbase =
+      p.w6 + ((long long)ph * taps * nchunks) * p.Cout * 48 + (long long)co0 * 48;
+  const long long wslab = (long long)p.Cout * 48;
+  const int lin = p.Lin;
+
+  int a_row[A_PT], a_k[A_PT], b_off[B_PT], b_lds[B_PT];
+#pragma unroll
+  for (int i = 0; i < A_PT; ++i) {
+    const int idx = group * A_H + min(gt + 256 * i, A_H - 1);
+    a_row[i] = idx / 6;
+    a_k[i] = idx - a_row[i] * 6;
+  }
+#pragma unroll
+  for (int i = 0; i < B_PT; ++i) {
+    const int idx = group * B_H + min(gt + 256 * i, B_H - 1);
+    const int col = idx / 6, piece = idx - col * 6;
+    b_off[i] = idx * 8;
+    b_lds[i] = col * XROW + piece * 8;
+  }
+  f32x4 ra[2][A_PT], rb[2][B_PT];
+  auto loadA = [&](int c, f32x4(&r)[A_PT]) {
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) {
+      const int ir = row0 + a_row[i];
+      const bool ok = ir >= 0 && ir < lin;
+      const unsigned short* src =
+          ok ? xb6 + (long long)ir * ldx6 + c * 48 + a_k[i] * 8 : reinterpret_cast<const unsigned short*>(g_zero_row);
+      r[i] = *reinterpret_cast<const f32x4*>(src);
+    }
+  };
+  auto storeA = [&](int buf, const f32x4(&r)[A_PT]) {
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i)
+      *reinterpret_cast<f32x4*>(lds + buf * ABUF + a_row[i] * XROW + a_k[i] * 8) = r[i];
+  };
+  auto loadB = [&](int c, int m, f32x4(&r)[B_PT]) {
+    const unsigned short* src = wbase + ((long long)m * nchunks + c) * wslab;
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) r[i] = *reinterpret_cast<const f32x4*>(src + b_off[i]);
+  };
+  auto storeB = [&](int slot, const f32x4(&r)[B_PT]) {
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) *reinterpret_cast<f32x4*>(lds + 2 * ABUF + slot * BBUF + b_lds[i]) = r[i];
+  };
+
+  const int lrow = lane & 31, hoff = (lane >> 5) * 24;
+  s16x8 af[TM][3], bfr[TN][3];
+  auto readF = [&](int c, int m, int slot) {
+    const int off = m * p.in_step - lo_rel;
+    const unsigned short* A = lds + (c & 1) * ABUF;
+    const unsigned short* Bsm = lds + 2 * ABUF + slot * BBUF;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const unsigned short* ap = A + (wm * WR + i * 32 + lrow + off) * XROW + hoff;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) af[i][pl] = *reinterpret_cast<const s16x8*>(ap + pl * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const unsigned short* bp = Bsm + (wn * WC + j * 32 + lrow) * XROW + hoff;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = *reinterpret_cast<const s16x8*>(bp + pl * 8);
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // MFMA cluster of one step with the staging loads `ld` spread through it: NL loads, one after
+  // every 24 / (NL + 1) MFMAs (sched_group_barrier pins the order), so their issue overlaps MFMAs
+  // instead of holding back the first one
+  auto mfma_with = [&](auto nl_tag, auto&& ld) {
+    constexpr int NL = decltype(nl_tag)::value;
+    __builtin_amdgcn_s_setprio(1);
+    ld();
+#define DCX_MF(i, j, x, y) \
+  acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[i][x]), \
+                                                      __builtin_bit_cast(bf16x8, bfr[j][y]), acc[i][j], 0, 0, 0)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        DCX_MF(i, j, 2, 0);
+        DCX_MF(i, j, 1, 1);
+        DCX_MF(i, j, 0, 2);
+        DCX_MF(i, j, 1, 0);
+        DCX_MF(i, j, 0, 1);
+        DCX_MF(i, j, 0, 0);
+      }
+#undef DCX_MF
+    if constexpr (NL > 0) {
+      constexpr int G = 24 / (NL + 1);
+#pragma unroll
+      for (int k = 0; k < NL; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, G, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 24 - NL * G, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto adv = [&](int& c_, int& m_) {
+    if (++m_ == taps) { m_ = 0; ++c_; }
+  };
+  // loads of step (cl, ml) into register set Q: the input chunk when the step opens one (1-tap:
+  // every step, clamped past the end, so unconditional), then the weight tile (clamped past the
+  // end, unconditional).  With a halo the input-chunk loads go out before the MFMA cluster and
+  // only the weight loads are spread through it.
+  int cl, ml;
+  constexpr int NL = HALO ? B_PT : A_PT + B_PT;
+  auto load_pre = [&](auto qtag) {
+    constexpr int Q = decltype(qtag)::value;
+    if constexpr (HALO > 0)
+      if (ml == 0 && cl < nchunks) loadA(cl, ra[Q]);
+  };
+  auto load_in = [&](auto qtag) {
+    constexpr int Q = decltype(qtag)::value;
+    return [&]() {
+      if constexpr (HALO == 0) loadA(min(cl, nchunks - 1), ra[Q]);
+      loadB(min(cl, nchunks - 1), cl < nchunks ? ml : taps - 1, rb[Q]);
+    };
+  };
+  auto load_step = [&](auto qtag) {  // prologue: plain
+    constexpr int Q = decltype(qtag)::value;
+    if (ml == 0 && cl < nchunks) loadA(cl, ra[Q]);
+    loadB(min(cl, nchunks - 1), cl < nchunks ? ml : taps - 1, rb[Q]);
+    adv(cl, ml);
+  };
+
+  // ---- prologue: steps 0 and 1 to LDS, step 2 into register set 0
+  loadA(0, ra[0]);
+  loadB(0, 0, rb[0]);
+  storeA(0, ra[0]);
+  storeB(0, rb[0]);
+  int c1 = 0, m1 = 0;  // position of step 1
+  adv(c1, m1);
+  loadB(c1, m1, rb[1]);
+  if (m1 == 0) loadA(1, ra[1]);  // taps == 1
+  storeB(1, rb[1]);
+  if (m1 == 0) storeA(1, ra[1]);
+  cl = c1;
+  ml = m1;
+  adv(cl, ml);                   // step 2
+  int cw = cl, mw = ml;          // next step this group stores: 2
+  load_step(std::integral_constant<int, 0>{});  // step 2 -> set 0; next load: step 3
+  __syncthreads();
+#ifdef DCX_CLOCK_DIAG
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  int cr = 0, mr = 0;
+  if (group == 0) {
+    readF(0, 0, 0);
+    adv(cr, mr);
+    // iteration s: MFMA(s) (after loading step s+3 into set (s+1) & 1), then MEM0(s): fragments
+    // of step s+1, store step s+2 from set s & 1
+    auto iter = [&](int s, auto qtag) {
+      constexpr int Q = decltype(qtag)::value;  // s & 1
+      load_pre(std::integral_constant<int, 1 - Q>{});
+      mfma_with(std::integral_constant<int, NL>{}, load_in(std::integral_constant<int, 1 - Q>{}));
+      adv(cl, ml);
+      __syncthreads();
+      if (s + 1 < nsteps) readF(cr, mr, (s + 1) & 1);
+      if (s + 2 < nsteps) {
+        storeB((s + 2) & 1, rb[Q]);
+        if (mw == 0) storeA(cw & 1, ra[Q]);
+      }
+      adv(cr, mr);
+      adv(cw, mw);
+      __syncthreads();
+    };
+    for (int s = 0; s < nsteps; s += 2) {
+      iter(s, std::integral_constant<int, 0>{});
+      iter(s + 1, std::integral_constant<int, 1>{});
+    }
+  } else {
+    // iteration s: MEM1(s): fragments of step s, store step s+1 from set (s+1) & 1 (step 1 came
+    // from the prologue); then MFMA(s) after loading step s+3 into set (s+1) & 1
+    auto iter = [&](int s, auto qtag) {
+      constexpr int Q = decltype(qtag)::value;  // s & 1
+      readF(cr, mr, s & 1);
+      if (s >= 1 && s + 1 < nsteps) {
+        storeB((s + 1) & 1, rb[1 - Q]);
+        if (mw == 0) storeA(cw & 1, ra[1 - Q]);
+      }
+      if (s >= 1) adv(cw, mw);
+      adv(cr, mr);
+      __syncthreads();
+      load_pre(std::integral_constant<int, 1 - Q>{});
+      mfma_with(std::integral_constant<int, NL>{}, load_in(std::integral_constant<int, 1 - Q>{}));
+      adv(cl, ml);
+      __syncthreads();
+    };
+    for (int s = 0; s < nsteps; s += 2) {
+      iter(s, std::integral_constant<int, 0>{});
+      iter(s + 1, std::integral_constant<int, 1>{});
     }
   }
 #ifdef DCX_CLOCK_DIAG
@@ -972,10 +1306,17 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
 
 template <int HALO>
 static hipError_t launch_x6pp(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
-  // (BN = 256 needs 128 accumulator + 72 fragment VGPRs and spills at 2 waves per SIMD)
-  const int mtiles = (p.Lq + 255) / 256;
-  if (kname) *kname = HALO ? "conv_gemm_x6pp<256,128,halo>" : "conv_gemm_x6pp<256,128>";
-  hipLaunchKernelGGL((conv_gemm_x6pp<HALO, 128>), dim3(mtiles * (p.Cout / 128), batch, phases), dim3(512), 0, s, p);
+  // (BN = 256 needs 128 accumulator + 72 fragment VGPRs and spills at 2 waves per SIMD).  1-tap
+  // convs take conv_gemm_x6lm (loads spread through the MFMA segments): 151 -> 161 TF/s at
+  // 1024 -> 4096; with a halo it measured equal at k11 and 4-5 % slower at k3 / taps 2.
+  const dim3 grid(((p.Lq + 255) / 256) * (p.Cout / 128), batch, phases);
+  if constexpr (HALO == 0) {
+    if (kname) *kname = "conv_gemm_x6lm<256,128>";
+    hipLaunchKernelGGL((conv_gemm_x6lm<0>), grid, dim3(512), 0, s, p);
+  } else {
+    if (kname) *kname = "conv_gemm_x6pp<256,128,halo>";
+    hipLaunchKernelGGL((conv_gemm_x6pp<HALO, 128>), grid, dim3(512), 0, s, p);
+  }
   return hipGetLastError();
 }
 

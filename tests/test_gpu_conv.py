@@ -28,6 +28,9 @@ CASES = [
     (256, 128, 4, 1, True, 2, 129),
     (64, 32, 4, 1, True, 2, 333),
     (1024, 1024, 1, 1, True, 1, 45),
+    # fewer K16 steps than the LDS-DMA prefetch depth (2 and 6 steps)
+    (32, 128, 1, 1, False, 1, 300),
+    (32, 256, 3, 1, False, 1, 200),
 ]
 
 

@@ -24,8 +24,8 @@ def short(name):
     if base == "conv_gemm_f32":
         kind = "vq_dist_argmin_f32" if parts[-1] == "true" else "conv_gemm_f32"
         return f"{kind}<{parts[0]},{parts[1]}>"
-    if base == "conv_gemm_x6pp":
-        return "conv_gemm_x6pp<256,128,halo>" if parts and parts[0] != "0" else "conv_gemm_x6pp<256,128>"
+    if base in ("conv_gemm_x6pp", "conv_gemm_x6lm"):
+        return f"{base}<256,128,halo>" if parts and parts[0] != "0" else f"{base}<256,128>"
     if base == "vq_prefilter_x3":
         kind = "vq_prefilter_x3" if len(parts) < 5 or parts[4] == "true" else "vq_prefilter_x2"
         return f"{kind}<{parts[0]},{parts[1]}>"
