@@ -135,6 +135,9 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, f32x16 (&acc)[
   const int c4 = (tid % (BN / 4)) * 4, trow = tid / (BN / 4), co = co0 + c4;
   const f32x4 bias4 = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 gamma4 = p.epi == EPI_GAMMA_RES ? *reinterpret_cast<const f32x4*>(p.gamma + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+#ifdef DCX_DIAG_NOEPI
+  if (q0 >= 0) return;  // timing-only build: main loop without the epilogue
+#endif
 #pragma unroll 1
   for (int r0 = 0; r0 < BM; r0 += RPP) {
     __syncthreads();
@@ -1321,6 +1324,256 @@ static hipError_t launch_x6pp(const ConvParams& p, int batch, int phases, hipStr
 }
 
 // ---------------------------------------------------------------------------------------------
+// conv_gemm_x6dm: ping-pong x6 conv on 256 x 256 (or 512 x 128) tiles with LDS-DMA staging.
+//
+// conv_gemm_x6pp's per-segment stamps put its memory segment (12 fragment reads, register-staged
+// LDS stores, global loads: ~1050 cycles at k11) above its MFMA segment (24 MFMAs, ~800), so the
+// matrix pipe waited at every barrier.  Here:
+//  * staging is LDS-DMA (buffer_load_dwordx4 ... lds): no staging registers and no ds_write
+//    pass in the memory segment; each wave issues its pieces and retires them one segment later
+//    with a counted vmcnt;
+//  * the freed registers buy 64 x 128 wave tiles (256 x 256 block tile): 48 MFMAs per segment
+//    against 18 fragment reads (a quarter fewer LDS reads per MFMA than 64 x 64), and each input
+//    tile is re-read by half as many column tiles.
+// LDS images are lane-linear per DMA instruction (1 KiB = 64 x 16 B): the unpadded 96-byte rows
+// of XRow<true> (rows with bit 3 set hold their two K halves swapped, conflict-free fragment
+// reads at any tap offset), the swizzle applied on the per-lane SOURCE offsets.  Out-of-range
+// input rows (the conv's zero padding) are out of the buffer descriptor's range and load zeros.
+// Ring: 3 weight slots (step t in slot t % 3) and 2 input-chunk buffers (chunk parity); step t
+// is issued by group 0 in MEM0(t - 3) and by group 1 in MEM1(t - 2), retired at the end of each
+// wave's next memory segment, first read in segment 2t - 1 (the schedule of conv_gemm_x6pp).
+// ---------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned short* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, voff, soff, 0, 0);
+}
+// barrier that keeps the compiler's memory ops on their side and does not drain the DMA queue
+__device__ __forceinline__ void seg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void wait_dma(int n) {  // n = DMA pieces this wave issued since the ones to retire
+#define DCX_W(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+  switch (n) {
+    DCX_W(1) DCX_W(2) DCX_W(3) DCX_W(4) DCX_W(5) DCX_W(6) DCX_W(7) DCX_W(8) DCX_W(9) DCX_W(10) DCX_W(11)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+#undef DCX_W
+}
+
+// BN = 256: 256 x 256 tiles, 64 x 128 wave tiles; BN = 128: 512 x 128 tiles, 128 x 64 wave tiles
+// (the same 48 MFMAs and 18 fragment reads per segment).
+template <int HALO, int BN>
+__global__ void __launch_bounds__(512, 2) conv_gemm_x6dm(const ConvParams p) {
+  constexpr int BM = 65536 / BN, WN = 2;
+  constexpr int WR = BM / 4, WC = BN / 2, TM = WR / 32, TN = WC / 32;
+  constexpr int XS = XRow<true>::kStride;  // 48 ushorts = 96-byte rows
+  // DMA instructions (1 KiB each) per group per tile; a group's instructions are dealt round-robin
+  // to its 4 waves.  Halo: input chunks double-buffered by chunk parity; 1-tap: every step opens a
+  // chunk, so the input tiles ride the weight ring's 3 slots.
+  constexpr int A_G = (BM + HALO) * 6 / 128, B_G = BN * 6 / 128;
+  constexpr int A_PW = (A_G + 3) / 4, B_PW = (B_G + 3) / 4;
+  constexpr int NA = HALO ? 2 : 3;
+  constexpr int ABUF = 2 * A_G * 512;  // ushorts
+  constexpr int BBUF = BN * XS;
+  constexpr int LDS_US = NA * ABUF + 3 * BBUF;
+  static_assert((BM + HALO) * 6 % 128 == 0 && 2 * B_G * 512 == BBUF && A_PW + B_PW <= 11, "DMA piece counts");
+  static_assert(LDS_US * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned short lds[LDS_US];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int group = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntiles = p.Cout / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = wg / ntiles, nt = wg - mt * ntiles;
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int b = blockIdx.y, ph = blockIdx.z;
+  const int nchunks = p.Cin / BK;
+  const int taps = p.taps;
+  const int nsteps = nchunks * taps;
+  const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
+  const int row0 = q0 + p.in_base[ph] + lo_rel;
+  const int arow = p.ldx * 6;  // bytes per planes row
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.x6 + (long long)b * p.x_bstride * 3), 0, p.Lin * arow, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.w6 + (long long)ph * taps * nchunks * p.Cout * 48), 0, taps * nchunks * p.Cout * 96, 0x00020000);
+
+  // per-lane source offsets of this wave's pieces (lane-linear LDS, swizzle on the source); the
+  // wave's i-th instruction is its group's instruction i * 4 + gw
+  const int a_cnt = (A_G - gw + 3) / 4, b_cnt = (B_G - gw + 3) / 4;  // wave-uniform
+  int a_off[A_PW], b_off[B_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int P = (group * A_G + i * 4 + gw) * 64 + lane;
+    const int row = P / 6, s = P - row * 6;
+    const int hl = (s >= 3) ^ ((row >> 3) & 1), pl = s >= 3 ? s - 3 : s;
+    a_off[i] = (row0 + row) * arow + (hl * 3 + pl) * 16;  // negative rows: huge unsigned, out of range
+  }
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int P = (group * B_G + i * 4 + gw) * 64 + lane;
+    const int col = P / 6, s = P - col * 6;
+    const int sg = ((col >> 3) & 1) ? (s >= 3 ? s - 3 : s + 3) : s;
+    b_off[i] = (co0 + col) * 96 + sg * 16;
+  }
+  unsigned short* const a_dst = lds + (group * A_G + gw) * 512;
+  unsigned short* const b_dst = lds + NA * ABUF + (group * B_G + gw) * 512;
+  auto dmaA = [&](int c, int abuf) {
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i)
+      if (A_G % 4 == 0 || i < a_cnt) dma16(rx, a_dst + abuf * ABUF + i * 2048, a_off[i] + c * 96, 0);
+  };
+  auto dmaB = [&](int c, int m, int slot) {
+    const int soff = (m * nchunks + c) * p.Cout * 96;
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i)
+      if (B_G % 4 == 0 || i < b_cnt) dma16(rw, b_dst + slot * BBUF + i * 2048, b_off[i], soff);
+  };
+  // DMA of one step (its input chunk first when the step opens one); returns the pieces issued
+  auto dma_step = [&](int c, int m, int slot) {
+    int n = b_cnt;
+    if (m == 0) {
+      dmaA(c, HALO ? (c & 1) : slot);
+      n += a_cnt;
+    }
+    dmaB(c, m, slot);
+    return n;
+  };
+
+  const int lrow = lane & 31, h = lane >> 5;
+  s16x8 af[TM][3], bfr[TN][3];
+  auto readF = [&](int c, int m, int slot) {
+    const int off = m * p.in_step - lo_rel;
+    const unsigned short* A = lds + (HALO ? (c & 1) : slot) * ABUF;
+    const unsigned short* Bs = lds + NA * ABUF + slot * BBUF;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm * WR + i * 32 + lrow + off;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) af[i][pl] = *reinterpret_cast<const s16x8*>(A + XRow<true>::off(r, h * 3 + pl));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WC + j * 32 + lrow;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = *reinterpret_cast<const s16x8*>(Bs + XRow<true>::off(col, h * 3 + pl));
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  auto mfma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#define DCX_MF(i, j, x, y) \
+  acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[i][x]), \
+                                                      __builtin_bit_cast(bf16x8, bfr[j][y]), acc[i][j], 0, 0, 0)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        DCX_MF(i, j, 2, 0);
+        DCX_MF(i, j, 1, 1);
+        DCX_MF(i, j, 0, 2);
+        DCX_MF(i, j, 1, 0);
+        DCX_MF(i, j, 0, 1);
+        DCX_MF(i, j, 0, 0);
+      }
+#undef DCX_MF
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto adv = [&](int& c_, int& m_) {
+    if (++m_ == taps) { m_ = 0; ++c_; }
+  };
+  auto inc3 = [](int& slot) { slot = slot == 2 ? 0 : slot + 1; };
+
+  // ---- prologue: steps 0, 1, 2 (both groups their pieces), drained
+  int cl = 0, ml = 0;
+  for (int t = 0; t < 3; ++t) {
+    if (t < nsteps) dma_step(cl, ml, t);
+    adv(cl, ml);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  seg_barrier();
+#ifdef DCX_CLOCK_DIAG
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  // cl, ml: step 3, the next step either group issues
+  int cr = 0, mr = 0;
+  if (group == 0) {
+    readF(0, 0, 0);
+    adv(cr, mr);
+    int rs = 1, ws = 0;  // slot of the step read next (s + 1), of the step issued next (s + 3)
+    for (int s = 0; s < nsteps; ++s) {
+      mfma();  // MFMA(s)
+      seg_barrier();
+      // MEM0(s): fragments of step s + 1, issue step s + 3, retire step s + 2
+      if (s + 1 < nsteps) readF(cr, mr, rs);
+      int n = 0;
+      if (s + 3 < nsteps) n = dma_step(cl, ml, ws);
+      wait_dma(n);
+      seg_barrier();
+      adv(cr, mr);
+      adv(cl, ml);
+      inc3(rs);
+      inc3(ws);
+    }
+  } else {
+    int rs = 0, ws = 0;  // slot of step s, of step s + 2
+    for (int s = 0; s < nsteps; ++s) {
+      // MEM1(s): fragments of step s, issue step s + 2 (s >= 1), retire step s + 1
+      readF(cr, mr, rs);
+      int n = 0;
+      if (s >= 1 && s + 2 < nsteps) {
+        n = dma_step(cl, ml, ws);
+        adv(cl, ml);
+      }
+      wait_dma(n);
+      seg_barrier();
+      mfma();  // MFMA(s)
+      seg_barrier();
+      adv(cr, mr);
+      inc3(rs);
+      if (s >= 1) inc3(ws);
+      else ws = 0;  // step 3's slot
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef DCX_CLOCK_DIAG
+  if (threadIdx.x == 0) {  // steps counted in units of x6pp's (half the MFMAs)
+    atomicAdd(&g_clock_diag[0], __builtin_amdgcn_s_memtime() - t0);
+    atomicAdd(&g_clock_diag[1], __builtin_amdgcn_s_memrealtime() - r0);
+    atomicAdd(&g_clock_diag[2], 2ull * nsteps);
+  }
+#endif
+  epilogue_lds<BM, BN, 4, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+}
+
+// whether conv_gemm_x6dm takes the conv: planes input, Cout % 256, taps >= 2 with a halo or one
+// tap without, and 32-bit buffer offsets for the input rows (with the tile's halo) and the weights
+static bool x6dm_ok(const ConvParams& p, bool halo, int bn) {
+  if (!p.x6 || !p.w6 || p.nprod != 6 || p.Cout % bn || (halo ? p.taps < 2 : p.taps != 1)) return false;
+  const long long arow = (long long)p.ldx * 6;
+  const long long wbytes = (long long)p.taps * (p.Cin / BK) * p.Cout * 96;
+  return (long long)(p.Lin + 1024) * arow < (1LL << 31) && 1024 * arow < (1LL << 31) && wbytes < (1LL << 31);
+}
+
+template <int HALO, int BN>
+static hipError_t launch_x6dm(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
+  constexpr int BM = 65536 / BN;
+  const dim3 grid(((p.Lq + BM - 1) / BM) * (p.Cout / BN), batch, phases);
+  if (kname)
+    *kname = BN == 256 ? (HALO ? "conv_gemm_x6dm<256,256,halo>" : "conv_gemm_x6dm<256,256>") : "conv_gemm_x6dm<512,128,halo>";
+  hipLaunchKernelGGL((conv_gemm_x6dm<HALO, BN>), grid, dim3(512), 0, s, p);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // VQ prefilter GEMM (x6 mode): approximate x.e from hi*hi + hi*mid + mid*hi of the planes
 // (bound in launch_vq_prefilter), per-tile top 2 of (x2 + e2) - 2 x.e (epilogue_top2).
 //
@@ -1560,6 +1813,9 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       name("conv_gemm_x6w4f<256,32,halo>", "conv_gemm_bf16w4f<256,32,halo>");
       return launch_x6w8_af32<256, 32, 4, 1, 64>(p, batch, phases, s);
     }
+#ifndef DCX_NO_DM
+    if (!h && x6dm_ok(p, false, 256)) return launch_x6dm<0, 256>(p, batch, phases, s, kname);  // x6 1-tap, Cout % 256
+#endif
 #ifndef DCX_NO_PP
     if (p.Cout % 128 == 0 && !h && !b1) return launch_x6pp<0>(p, batch, phases, s, kname);  // x6 1-tap
 #endif
@@ -1568,6 +1824,10 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       return launch_x6w8<128, 128, 2, 2, 0, false>(p, batch, phases, s);
     }
     if (p.Cout % 128 == 0) {
+#ifndef DCX_NO_DM
+      if (x6dm_ok(p, true, 256)) return launch_x6dm<64, 256>(p, batch, phases, s, kname);  // LDS-DMA ping-pong
+      if (x6dm_ok(p, true, 128)) return launch_x6dm<64, 128>(p, batch, phases, s, kname);
+#endif
 #ifndef DCX_NO_PP
       if (!b1) return launch_x6pp<64>(p, batch, phases, s, kname);  // x6: ping-pong kernel
 #endif

@@ -31,6 +31,11 @@ CASES = [
     # fewer K16 steps than the LDS-DMA prefetch depth (2 and 6 steps)
     (32, 128, 1, 1, False, 1, 300),
     (32, 256, 3, 1, False, 1, 200),
+    # 256-column LDS-DMA kernel: 2 steps (ConvT phases), 12 steps with dilation
+    (16, 256, 4, 1, True, 2, 100),
+    (64, 512, 3, 2, False, 1, 260),
+    # 512-row tiles (Cout 128): three row tiles, the last ragged
+    (128, 128, 3, 1, False, 1, 1100),
 ]
 
 
