@@ -115,11 +115,14 @@ extern "C" int dcx_diag_seg(unsigned long long* out13, int reset) {
 // loads of bias / gamma / residual / mean accumulator and 16-byte fp32 stores (8-byte plane
 // stores).  This keeps the per-element code out of the 64-way unrolled accumulator loop.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int LDS_FLOATS, int NT>
-__device__ __forceinline__ void epilogue_lds(const ConvParams& p, f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int q0,
-                                             int co0, int b, int ph, float* smem) {
+// acc: f32x16[WR/32][WC/32] (32x32 MFMA blocks) or f32x4[WR/16][WC/16] (16x16 blocks).
+template <int BM, int BN, int WM, int WN, int LDS_FLOATS, int NT, typename AccT>
+__device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int q0, int co0, int b, int ph,
+                                             float* smem) {
   constexpr int WR = BM / WM, WC = BN / WN;
   constexpr int TM = WR / 32, TN = WC / 32;
+  constexpr bool M16 = sizeof(acc[0][0]) == 16;
+  static_assert(sizeof(acc) == WR * WC * 4 / 64, "accumulator tile");
   constexpr int LDSW = BN + 4;
   constexpr int RPP = (BM * LDSW <= LDS_FLOATS) ? BM
                       : (BM / 2 * LDSW <= LDS_FLOATS) ? BM / 2
@@ -142,15 +145,27 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, f32x16 (&acc)[
   for (int r0 = 0; r0 < BM; r0 += RPP) {
     __syncthreads();
     if (wm * WR >= r0 && wm * WR < r0 + RPP) {
+      if constexpr (M16) {  // 16x16 block: lane holds column l & 15, rows 4 (l >> 4) + e
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < WR / 16; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+          for (int j = 0; j < WC / 16; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + rhalf - r0;
-            smem[row * LDSW + wn * WC + j * 32 + lrow] = acc[i][j][r];
-          }
+            for (int e = 0; e < 4; ++e) {
+              const int row = wm * WR + i * 16 + 4 * (lane >> 4) + e - r0;
+              smem[row * LDSW + wn * WC + j * 16 + (lane & 15)] = acc[i][j][e];
+            }
+      } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + rhalf - r0;
+              smem[row * LDSW + wn * WC + j * 32 + lrow] = acc[i][j][r];
+            }
+      }
     }
     __syncthreads();
     // Each thread always finishes the same 4 output channels (NT is a multiple of BN / 4), so
@@ -1554,6 +1569,252 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6dm(const ConvParams p) {
   epilogue_lds<BM, BN, 4, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
+// ---------------------------------------------------------------------------------------------
+// conv_gemm_x6dq: conv_gemm_x6dm on v_mfma_f32_16x16x32_bf16.
+//
+// The chip holds a lower clock under 32x32x16 MFMA load than under 16x16x32 at the same cycles per
+// FLOP (MI355X_MICROARCH.md, DVFS item 7), and x6dm's loop runs at ~95 % MFMA issue, so what is
+// left is the clock.  The six products of a K16 step fold into three K32 MFMAs by pairing terms in
+// the K dimension: k = (t, c) with t = lane >> 5 selecting the term, c the channel (lane bits 4
+// and 0-3 the channel half and row), so one MFMA sums x_t0 * y_t0 + x_t1 * y_t1 over 16 channels:
+//   A{h,m} . B{h',m'} = hh' + mm',   A{m,h} . B{h',m'} = mh' + hm',   A{l,h} . B{h',l'} = lh' + hl'.
+// Each operand set is one ds_read_b128 whose lanes pick their plane by t: 3 A sets per 16-row
+// block, 2 B sets per 16-column block.  A 64 x 128 (128 x 64) wave tile holds 8 x 4 (4 x 8) f32x4
+// accumulators; B fragments for the whole tile and the A fragments of RH row blocks fit in
+// registers, the MFMA segment reading the later row blocks' A itself behind the MFMAs of the
+// earlier ones.  A is then read in both segments of a step, so the input chunk buffer is reused
+// one segment later than in x6dm: taps >= 3 (the ResBlock and conv_pre convs).
+// LDS images: 16-row blocks, piece-major inside a block: 16-byte unit (r >> 4) * 96 + s * 16 +
+// (r & 15) for piece s = half * 3 + plane of row r; every ds_read_b128 then touches 16
+// consecutive rows of one piece per lane group (conflict-free at any tap offset).
+// ---------------------------------------------------------------------------------------------
+template <int BN>
+__global__ void __launch_bounds__(512, 2) conv_gemm_x6dq(const ConvParams p) {
+  constexpr int HALO = 64;
+  constexpr int BM = 65536 / BN, WN = 2;
+  constexpr int WR = BM / 4, WC = BN / 2, TM = WR / 16, TN = WC / 16;
+  constexpr int RH = BN == 256 ? 2 : 4;  // A row blocks held from the memory segment
+  constexpr int A_G = (BM + HALO) * 6 / 128, B_G = BN * 6 / 128;
+  constexpr int A_PW = (A_G + 3) / 4, B_PW = (B_G + 3) / 4;
+  constexpr int ABUF = 2 * A_G * 512;  // ushorts
+  constexpr int BBUF = BN * 48;
+  constexpr int LDS_US = 2 * ABUF + 3 * BBUF;
+  static_assert((BM + HALO) * 6 % 128 == 0 && 2 * B_G * 512 == BBUF && A_PW + B_PW <= 11, "DMA piece counts");
+  static_assert(LDS_US * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned short lds[LDS_US];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int group = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntiles = p.Cout / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = wg / ntiles, nt = wg - mt * ntiles;
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int b = blockIdx.y, ph = blockIdx.z;
+  const int nchunks = p.Cin / BK;
+  const int taps = p.taps;
+  const int nsteps = nchunks * taps;
+  const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
+  const int row0 = q0 + p.in_base[ph] + lo_rel;
+  const int arow = p.ldx * 6;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.x6 + (long long)b * p.x_bstride * 3), 0, p.Lin * arow, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.w6 + (long long)ph * taps * nchunks * p.Cout * 48), 0, taps * nchunks * p.Cout * 96, 0x00020000);
+
+  // DMA pieces: unit u of a tile image -> row (u / 96) * 16 + (u & 15), piece (u % 96) >> 4
+  const int a_cnt = (A_G - gw + 3) / 4, b_cnt = (B_G - gw + 3) / 4;
+  int a_off[A_PW], b_off[B_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int u = (group * A_G + i * 4 + gw) * 64 + lane;
+    const int blk = u / 96, rem = u - blk * 96;
+    a_off[i] = (row0 + blk * 16 + (rem & 15)) * arow + (rem >> 4) * 16;  // negative rows: out of range
+  }
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int u = (group * B_G + i * 4 + gw) * 64 + lane;
+    const int blk = u / 96, rem = u - blk * 96;
+    b_off[i] = (co0 + blk * 16 + (rem & 15)) * 96 + (rem >> 4) * 16;
+  }
+  unsigned short* const a_dst = lds + (group * A_G + gw) * 512;
+  unsigned short* const b_dst = lds + 2 * ABUF + (group * B_G + gw) * 512;
+  auto dma_step = [&](int c, int m, int slot) {
+    int n = b_cnt;
+    if (m == 0) {
+#pragma unroll
+      for (int i = 0; i < A_PW; ++i)
+        if (A_G % 4 == 0 || i < a_cnt) dma16(rx, a_dst + (c & 1) * ABUF + i * 2048, a_off[i] + c * 96, 0);
+      n += a_cnt;
+    }
+    const int soff = (m * nchunks + c) * p.Cout * 96;
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i)
+      if (B_G % 4 == 0 || i < b_cnt) dma16(rw, b_dst + slot * BBUF + i * 2048, b_off[i], soff);
+    return n;
+  };
+
+  // fragment sets: lane picks plane by t = lane >> 5, channel half hf = (lane >> 4) & 1
+  const int l15 = lane & 15, hf = (lane >> 4) & 1, t = lane >> 5;
+  const int soA0 = (hf * 3 + t) * 256, soA1 = (hf * 3 + (t ? 0 : 1)) * 256, soA2 = (hf * 3 + (t ? 0 : 2)) * 256;
+  const int soB0 = (hf * 3 + t) * 256, soB1 = (hf * 3 + (t ? 2 : 0)) * 256;  // bytes (piece stride 256)
+  const char* const ldsb = reinterpret_cast<const char*>(lds);
+  const int bcol = (wn * WC / 16) * 1536 + l15 * 16 + 4 * ABUF;  // bytes, B image of slot 0
+  s16x8 aq[RH][3], bq[TN][2];
+  int abase = 0;  // bytes: this lane's row in the A image of the step being read
+  auto readA1 = [&](int rb, int k, int set) {
+    const char* a = ldsb + abase + rb * 1536 + (set == 0 ? soA0 : set == 1 ? soA1 : soA2);
+    aq[k][set] = *reinterpret_cast<const s16x8*>(a);
+  };
+  auto readA = [&](int rb, int k) {
+    readA1(rb, k, 0);
+    readA1(rb, k, 1);
+    readA1(rb, k, 2);
+  };
+  auto readF = [&](int c, int m, int slot) {
+    const int r = wm * WR + m * p.in_step - lo_rel + l15;
+    abase = (c & 1) * ABUF * 2 + (r >> 4) * 1536 + (r & 15) * 16;
+    const char* bb = ldsb + bcol + slot * BBUF * 2;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bq[j][0] = *reinterpret_cast<const s16x8*>(bb + j * 1536 + soB0);
+      bq[j][1] = *reinterpret_cast<const s16x8*>(bb + j * 1536 + soB1);
+    }
+#pragma unroll
+    for (int k = 0; k < RH; ++k) readA(k, k);
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // MFMA segment: row block by row block, and within a block operand set by operand set (per
+  // accumulator: lh' + hl', then mh' + hm', then hh' + mm'); as soon as a set's MFMAs are issued,
+  // its registers take the same set of row block rb + RH (read from the same step's image), so the
+  // reads are spread through the segment and land 2..3 sets' worth of MFMAs before their use
+  auto mfma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int rb = 0; rb < TM; ++rb) {
+      const int k = rb % RH;
+#pragma unroll
+      for (int set = 2; set >= 0; --set) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[rb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, aq[k][set]),
+                                                               __builtin_bit_cast(bf16x8, bq[j][set == 2 ? 1 : 0]),
+                                                               acc[rb][j], 0, 0, 0);
+        if (rb + RH < TM) readA1(rb + RH, k, set);
+      }
+    }
+#pragma unroll
+    for (int rb = 0; rb < TM; ++rb)
+#pragma unroll
+      for (int set = 0; set < 3; ++set) {
+        __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);
+        if (rb + RH < TM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto adv = [&](int& c_, int& m_) {
+    if (++m_ == taps) { m_ = 0; ++c_; }
+  };
+  auto inc3 = [](int& slot) { slot = slot == 2 ? 0 : slot + 1; };
+
+  int cl = 0, ml = 0;
+  for (int tt = 0; tt < 3; ++tt) {
+    if (tt < nsteps) dma_step(cl, ml, tt);
+    adv(cl, ml);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  seg_barrier();
+#ifdef DCX_CLOCK_DIAG
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  int cr = 0, mr = 0;
+#ifdef DCX_SEG_DIAG
+  unsigned long long sd[4] = {};
+#endif
+  if (group == 0) {
+    readF(0, 0, 0);
+    adv(cr, mr);
+    int rs = 1, ws = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      DCX_SEGT(ta);
+      mfma();  // MFMA(s)
+      DCX_SEGT(tb);
+      seg_barrier();
+      DCX_SEGT(tc);
+      if (s + 1 < nsteps) readF(cr, mr, rs);
+      int n = 0;
+      if (s + 3 < nsteps) n = dma_step(cl, ml, ws);
+      wait_dma(n);
+      DCX_SEGT(td);
+      seg_barrier();
+      DCX_SEGT(te);
+#ifdef DCX_SEG_DIAG
+      sd[0] += tb - ta; sd[1] += tc - tb; sd[2] += td - tc; sd[3] += te - td;
+#endif
+      adv(cr, mr);
+      adv(cl, ml);
+      inc3(rs);
+      inc3(ws);
+    }
+  } else {
+    int rs = 0, ws = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      DCX_SEGT(ta);
+      readF(cr, mr, rs);
+      int n = 0;
+      if (s >= 1 && s + 2 < nsteps) {
+        n = dma_step(cl, ml, ws);
+        adv(cl, ml);
+      }
+      wait_dma(n);
+      DCX_SEGT(tb);
+      seg_barrier();
+      DCX_SEGT(tc);
+      mfma();  // MFMA(s)
+      DCX_SEGT(td);
+      seg_barrier();
+      DCX_SEGT(te);
+#ifdef DCX_SEG_DIAG
+      sd[2] += tb - ta; sd[3] += tc - tb; sd[0] += td - tc; sd[1] += te - td;
+#endif
+      adv(cr, mr);
+      inc3(rs);
+      if (s >= 1) inc3(ws);
+      else ws = 0;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef DCX_SEG_DIAG
+  if ((threadIdx.x & 255) == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) atomicAdd(&g_seg_diag[group * 6 + i], sd[i]);
+    if (group == 0) atomicAdd(&g_seg_diag[12], (unsigned long long)nsteps);
+  }
+#endif
+#ifdef DCX_CLOCK_DIAG
+  if (threadIdx.x == 0) {
+    atomicAdd(&g_clock_diag[0], __builtin_amdgcn_s_memtime() - t0);
+    atomicAdd(&g_clock_diag[1], __builtin_amdgcn_s_memrealtime() - r0);
+    atomicAdd(&g_clock_diag[2], 2ull * nsteps);
+  }
+#endif
+  epilogue_lds<BM, BN, 4, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+}
+
+template <int BN>
+static hipError_t launch_x6dq(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
+  constexpr int BM = 65536 / BN;
+  const dim3 grid(((p.Lq + BM - 1) / BM) * (p.Cout / BN), batch, phases);
+  if (kname) *kname = BN == 256 ? "conv_gemm_x6dq<256,256,halo>" : "conv_gemm_x6dq<512,128,halo>";
+  hipLaunchKernelGGL((conv_gemm_x6dq<BN>), grid, dim3(512), 0, s, p);
+  return hipGetLastError();
+}
+
 // whether conv_gemm_x6dm takes the conv: planes input, Cout % 256, taps >= 2 with a halo or one
 // tap without, and 32-bit buffer offsets for the input rows (with the tile's halo) and the weights
 static bool x6dm_ok(const ConvParams& p, bool halo, int bn) {
@@ -1824,6 +2085,10 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       return launch_x6w8<128, 128, 2, 2, 0, false>(p, batch, phases, s);
     }
     if (p.Cout % 128 == 0) {
+#ifndef DCX_NO_DQ
+      if (p.taps >= 3 && x6dm_ok(p, true, 256)) return launch_x6dq<256>(p, batch, phases, s, kname);  // 16x16x32
+      if (p.taps >= 3 && x6dm_ok(p, true, 128)) return launch_x6dq<128>(p, batch, phases, s, kname);
+#endif
 #ifndef DCX_NO_DM
       if (x6dm_ok(p, true, 256)) return launch_x6dm<64, 256>(p, batch, phases, s, kname);  // LDS-DMA ping-pong
       if (x6dm_ok(p, true, 128)) return launch_x6dm<64, 128>(p, batch, phases, s, kname);

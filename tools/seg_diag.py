@@ -44,7 +44,8 @@ def main():
         f(out, 1)
         st = max(out[12], 1)
         v = [out[i] / st for i in range(12)]
-        lab = ["mfma", "wait", "reads", "stores", "loads", "wait"]
+        lab = (["mfma", "wait", "mem", "wait", "-", "-"] if os.environ.get("DCX_SEG_DQ")
+               else ["mfma", "wait", "reads", "stores", "loads", "wait"])
         for g in range(2):
             print(f"{name:14s} g{g}: " + "  ".join(f"{lab[i]} {v[6 * g + i]:5.0f}" for i in range(6))
                   + f"  | step {sum(v[6 * g:6 * g + 6]):6.0f}", flush=True)
