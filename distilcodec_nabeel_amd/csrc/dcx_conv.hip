@@ -57,7 +57,9 @@ struct XRow {
   }
 };
 
-__device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
+// v * sigmoid(v) from v_exp_f32 and v_rcp_f32 (each ~1 ulp): 5 instructions instead of the
+// library expf and an IEEE divide; silu(-inf side) -> -0, silu(+large) -> v.
+__device__ __forceinline__ float silu_f(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
 __device__ __forceinline__ f32x4 round_bf16x4(f32x4 v) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) v[e] = bf16_val(bf16_bits(v[e]));

@@ -9,10 +9,9 @@ namespace dcx {
 
 typedef short s16x4p __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ unsigned short bf16_bits(float x) {
-  const unsigned u = __float_as_uint(x);
-  return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
-}
+// RNE to bf16: v_cvt_pk_bf16_f32 (hipcc pairs adjacent conversions into one instruction); the
+// same bits as (u + 0x7FFF + ((u >> 16) & 1)) >> 16 for every non-NaN input, NaN stays NaN.
+__device__ __forceinline__ unsigned short bf16_bits(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
 __device__ __forceinline__ float bf16_val(unsigned short b) { return __uint_as_float((unsigned)b << 16); }
 
 __device__ __forceinline__ void split3(float x, unsigned short& h, unsigned short& m, unsigned short& l) {
