@@ -175,7 +175,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "arith": ("fp32 operands split into 3 bf16 planes, 6 exact bf16 products per fp32 product, fp32 "
-                      "accumulation (v_mfma_f32_32x32x16_bf16)" if args.gemm == "x6" else
+                      "accumulation (v_mfma_f32_16x16x32_bf16 / 32x32x16_bf16)" if args.gemm == "x6" else
                       "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
             "data": "synthetic (speech/music-like 24 kHz clips; seeded synthetic weights, no checkpoint offline)",
             "config": {"workload": f"C2: {args.batch} x {args.seconds:g} s clips per GPU, full mel->encoder->VQ->"

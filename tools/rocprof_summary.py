@@ -26,6 +26,11 @@ def short(name):
         return f"{kind}<{parts[0]},{parts[1]}>"
     if base in ("conv_gemm_x6pp", "conv_gemm_x6lm"):
         return f"{base}<256,128,halo>" if parts and parts[0] != "0" else f"{base}<256,128>"
+    if base == "conv_gemm_x6dm":  # <HALO, BN>: BM = 65536 / BN
+        bm, bn = 65536 // int(parts[1]), int(parts[1])
+        return f"{base}<{bm},{bn},halo>" if parts[0] != "0" else f"{base}<{bm},{bn}>"
+    if base == "conv_gemm_x6dq":  # <BN>, halo
+        return f"{base}<{65536 // int(parts[0])},{parts[0]},halo>"
     if base == "vq_prefilter_x3":
         kind = "vq_prefilter_x3" if len(parts) < 5 or parts[4] == "true" else "vq_prefilter_x2"
         return f"{kind}<{parts[0]},{parts[1]}>"
