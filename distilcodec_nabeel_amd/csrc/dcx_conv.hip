@@ -1826,6 +1826,25 @@ static bool x6dm_ok(const ConvParams& p, bool halo, int bn) {
   return (long long)(p.Lin + 1024) * arow < (1LL << 31) && 1024 * arow < (1LL << 31) && wbytes < (1LL << 31);
 }
 
+// Whether the 64K-output tiles of the LDS-DMA kernels (BM x bn) beat 256 x 128 tiles of
+// conv_gemm_x6pp / x6lm for this launch.  Both run one workgroup per CU, so a launch takes
+// ceil(tiles / CUs) rounds; the smaller tiles take half the time at ~0.88 of the rate (measured on
+// the generator and encoder shapes).  Few-tile launches (short clips, the streaming hop, K-heavy
+// 1x1 convs with narrow outputs) keep the smaller tiles for their parallelism.
+static bool big_tiles_pay(const ConvParams& p, int batch, int phases, int bn) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+  }
+  const int bm = 65536 / bn;
+  const long long big = (long long)((p.Lq + bm - 1) / bm) * (p.Cout / bn) * batch * phases;
+  const long long small = (long long)((p.Lq + 255) / 256) * (p.Cout / 128) * batch * phases;
+  const double cost_big = (double)((big + cus - 1) / cus), cost_small = (double)((small + cus - 1) / cus) * 0.5 / 0.88;
+  return cost_big <= cost_small;
+}
+
 template <int HALO, int BN>
 static hipError_t launch_x6dm(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
   constexpr int BM = 65536 / BN;
@@ -2077,7 +2096,8 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       return launch_x6w8_af32<256, 32, 4, 1, 64>(p, batch, phases, s);
     }
 #ifndef DCX_NO_DM
-    if (!h && x6dm_ok(p, false, 256)) return launch_x6dm<0, 256>(p, batch, phases, s, kname);  // x6 1-tap, Cout % 256
+    if (!h && x6dm_ok(p, false, 256) && big_tiles_pay(p, batch, phases, 256))
+      return launch_x6dm<0, 256>(p, batch, phases, s, kname);  // x6 1-tap, Cout % 256
 #endif
 #ifndef DCX_NO_PP
     if (p.Cout % 128 == 0 && !h && !b1) return launch_x6pp<0>(p, batch, phases, s, kname);  // x6 1-tap
@@ -2087,13 +2107,16 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       return launch_x6w8<128, 128, 2, 2, 0, false>(p, batch, phases, s);
     }
     if (p.Cout % 128 == 0) {
+      const bool pay256 = big_tiles_pay(p, batch, phases, 256), pay128 = big_tiles_pay(p, batch, phases, 128);
+      (void)pay256;
+      (void)pay128;
 #ifndef DCX_NO_DQ
-      if (p.taps >= 3 && x6dm_ok(p, true, 256)) return launch_x6dq<256>(p, batch, phases, s, kname);  // 16x16x32
-      if (p.taps >= 3 && x6dm_ok(p, true, 128)) return launch_x6dq<128>(p, batch, phases, s, kname);
+      if (p.taps >= 3 && pay256 && x6dm_ok(p, true, 256)) return launch_x6dq<256>(p, batch, phases, s, kname);  // 16x16x32
+      if (p.taps >= 3 && pay128 && x6dm_ok(p, true, 128)) return launch_x6dq<128>(p, batch, phases, s, kname);
 #endif
 #ifndef DCX_NO_DM
-      if (x6dm_ok(p, true, 256)) return launch_x6dm<64, 256>(p, batch, phases, s, kname);  // LDS-DMA ping-pong
-      if (x6dm_ok(p, true, 128)) return launch_x6dm<64, 128>(p, batch, phases, s, kname);
+      if (pay256 && x6dm_ok(p, true, 256)) return launch_x6dm<64, 256>(p, batch, phases, s, kname);  // LDS-DMA ping-pong
+      if (pay128 && x6dm_ok(p, true, 128)) return launch_x6dm<64, 128>(p, batch, phases, s, kname);
 #endif
 #ifndef DCX_NO_PP
       if (!b1) return launch_x6pp<64>(p, batch, phases, s, kname);  // x6: ping-pong kernel
