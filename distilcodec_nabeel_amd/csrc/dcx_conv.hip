@@ -820,15 +820,19 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) conv_gemm_x6w8(const ConvPara
 // and 2t+2.  Input tiles are double-buffered by chunk parity and follow the schedule of their
 // chunk's first step.  Each group stages half of every tile (both halves with the same maps).
 // ---------------------------------------------------------------------------------------------
-template <int HALO, int BN>
+// AF32 (Cout = 64, fp32 input split while staging, as conv_gemm_x6w4f): 512 x 64 tiles, 8 x 1
+// waves with the same 64 x 64 wave tiles, so the staging VALU of one group overlaps the other
+// group's MFMAs.
+template <int HALO, int BN, bool AF32 = false>
 __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
   // wave tiles 64 x (BN / 2): 24 MFMAs per segment at BN = 128
-  static_assert(BN == 128 || BN == 256, "column tile");
-  constexpr int BM = 256, WN = 2;
+  static_assert(BN == 128 || BN == 256 || (AF32 && BN == 64), "column tile");
+  constexpr int BM = AF32 ? 512 : 256, WN = AF32 ? 1 : 2, WM = 8 / WN;
   constexpr int WR = 64, WC = BN / WN, TM = 2, TN = WC / 32;
   constexpr int XROW = 56;  // padded 112-byte rows
   constexpr int AROWS = BM + HALO;
-  constexpr int A_P = AROWS * 6, B_P = BN * 6;          // 16-byte pieces per tile
+  constexpr int APC = AF32 ? 4 : 6;  // staged 16-byte pieces per input row per chunk
+  constexpr int A_P = AROWS * APC, B_P = BN * 6;        // 16-byte pieces per tile
   constexpr int A_H = A_P / 2, B_H = B_P / 2;           // per group
   constexpr int A_PT = (A_H + 255) / 256, B_PT = (B_H + 255) / 256;
   constexpr int ABUF = AROWS * XROW, BBUF = BN * XROW;
@@ -843,7 +847,8 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
   const int b = blockIdx.y, ph = blockIdx.z;
-  const unsigned short* __restrict__ xb6 = p.x6 + (long long)b * p.x_bstride * 3;
+  const unsigned short* __restrict__ xb6 = AF32 ? nullptr : p.x6 + (long long)b * p.x_bstride * 3;
+  const float* __restrict__ xbf = AF32 ? p.x + (long long)b * p.x_bstride : nullptr;
   const long long ldx6 = (long long)p.ldx * 3;
   const int nchunks = p.Cin / BK;
   const int taps = p.taps;
@@ -860,8 +865,8 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
 #pragma unroll
   for (int i = 0; i < A_PT; ++i) {
     const int idx = group * A_H + min(gt + 256 * i, A_H - 1);
-    a_row[i] = idx / 6;
-    a_k[i] = idx - a_row[i] * 6;
+    a_row[i] = idx / APC;
+    a_k[i] = idx - a_row[i] * APC;  // AF32: 4-channel group
   }
 #pragma unroll
   for (int i = 0; i < B_PT; ++i) {
@@ -876,15 +881,37 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
     for (int i = 0; i < A_PT; ++i) {
       const int ir = row0 + a_row[i];
       const bool ok = ir >= 0 && ir < lin;
-      const unsigned short* src =
-          ok ? xb6 + (long long)ir * ldx6 + c * 48 + a_k[i] * 8 : reinterpret_cast<const unsigned short*>(g_zero_row);
-      ra[i] = *reinterpret_cast<const f32x4*>(src);
+      if constexpr (AF32) {
+        const float* src = ok ? xbf + (long long)ir * p.ldx + c * 16 + a_k[i] * 4 : g_zero_row;
+        ra[i] = *reinterpret_cast<const f32x4*>(src);
+      } else {
+        const unsigned short* src =
+            ok ? xb6 + (long long)ir * ldx6 + c * 48 + a_k[i] * 8 : reinterpret_cast<const unsigned short*>(g_zero_row);
+        ra[i] = *reinterpret_cast<const f32x4*>(src);
+      }
     }
   };
   auto storeA = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < A_PT; ++i)
-      *reinterpret_cast<f32x4*>(lds + buf * ABUF + a_row[i] * XROW + a_k[i] * 8) = ra[i];
+    for (int i = 0; i < A_PT; ++i) {
+      if constexpr (AF32) {  // silu (optional) and the 3-plane split of 4 channels: three 8-byte stores
+        s16x4 hv, mv, lv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          unsigned short hb, mb, lb;
+          split3(p.silu_in ? silu_f(ra[i][e]) : ra[i][e], hb, mb, lb);  // silu(0) = 0: padding stays 0
+          hv[e] = (short)hb;
+          mv[e] = (short)mb;
+          lv[e] = (short)lb;
+        }
+        unsigned short* d = lds + buf * ABUF + a_row[i] * XROW + (a_k[i] >> 1) * 24 + (a_k[i] & 1) * 4;
+        *reinterpret_cast<s16x4*>(d) = hv;
+        *reinterpret_cast<s16x4*>(d + 8) = mv;
+        *reinterpret_cast<s16x4*>(d + 16) = lv;
+      } else {
+        *reinterpret_cast<f32x4*>(lds + buf * ABUF + a_row[i] * XROW + a_k[i] * 8) = ra[i];
+      }
+    }
   };
   auto loadB = [&](int c, int m) {
     const unsigned short* src = wbase + ((long long)m * nchunks + c) * wslab;
@@ -1070,7 +1097,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
     atomicAdd(&g_clock_diag[2], (unsigned long long)nsteps);
   }
 #endif
-  epilogue_lds<BM, BN, 4, WN, (2 * ABUF + 2 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+  epilogue_lds<BM, BN, WM, WN, (2 * ABUF + 2 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2089,6 +2116,14 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
     if (!p.x6) {  // fp32 input, split while staging: small-Cout tiles only
       if (!p.x || p.Cin > 128 || p.Cout > 64 || p.taps < 2) return hipErrorInvalidValue;
       if (p.Cout == 64) {
+#ifndef DCX_NO_PF
+        if (!b1) {  // x6: ping-pong, 512 x 64 tiles
+          if (kname) *kname = "conv_gemm_x6pf<512,64,halo>";
+          hipLaunchKernelGGL((conv_gemm_x6pp<64, 64, true>), dim3(((p.Lq + 511) / 512) * (p.Cout / 64), batch, phases),
+                             dim3(512), 0, s, p);
+          return hipGetLastError();
+        }
+#endif
         name("conv_gemm_x6w4f<256,64,halo>", "conv_gemm_bf16w4f<256,64,halo>");
         return launch_x6w8_af32<256, 64, 4, 1, 64>(p, batch, phases, s);
       }

@@ -24,6 +24,8 @@ def short(name):
     if base == "conv_gemm_f32":
         kind = "vq_dist_argmin_f32" if parts[-1] == "true" else "conv_gemm_f32"
         return f"{kind}<{parts[0]},{parts[1]}>"
+    if base == "conv_gemm_x6pp" and len(parts) > 2 and parts[2] == "true":
+        return "conv_gemm_x6pf<512,64,halo>"
     if base in ("conv_gemm_x6pp", "conv_gemm_x6lm"):
         return f"{base}<256,128,halo>" if parts and parts[0] != "0" else f"{base}<256,128>"
     if base == "conv_gemm_x6dm":  # <HALO, BN>: BM = 65536 / BN
