@@ -323,6 +323,16 @@ __device__ __forceinline__ void epilogue_top2(const ConvParams& p, f32x16 (&acc)
   const int wm = wave / WN, wn = wave % WN;
   const int lrow = lane & 31;
   const int rhalf = 4 * (lane >> 5);
+  // every |x|^2 and |e|^2 this lane needs, loaded up front (unconditional, row index clamped: rows
+  // past Lq are never stored), so their latency is paid once rather than once per row
+  float xxv[TM][16], e2v[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      xxv[i][r] = p.x2[min(q0 + wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + rhalf, p.Lq - 1)];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) e2v[j] = p.e2[co0 + wn * WC + j * 32 + lrow];
   __syncthreads();
   float* rv = smem;                                      // [WN][BM]
   float* rv2 = smem + WN * BM;                           // [WN][BM]
@@ -332,14 +342,13 @@ __device__ __forceinline__ void epilogue_top2(const ConvParams& p, f32x16 (&acc)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rloc = wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + rhalf;
-      const int q = q0 + rloc;
-      const float xx = (q < p.Lq) ? p.x2[q] : 0.f;
+      const float xx = xxv[i][r];
       float v1 = __builtin_inff(), v2 = __builtin_inff();
       int i1 = 0x7fffffff;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int co = co0 + wn * WC + j * 32 + lrow;
-        const float d2 = (xx + p.e2[co]) + (-2.0f * acc[i][j][r]);
+        const float d2 = (xx + e2v[j]) + (-2.0f * acc[i][j][r]);
         top2_merge(v1, i1, v2, d2, co, __builtin_inff());
       }
 #pragma unroll
@@ -1917,7 +1926,7 @@ __global__ void __launch_bounds__(512) vq_prefilter_x3(const ConvParams p) {
   const int mt = (sup % nsm) * 16 + (xc & 3) * 4 + (l & 3);
   const int nt = (sup / nsm) * 16 + (xc >> 2) * 8 + (l >> 2);
   if (mt >= mtiles) return;  // whole workgroup, before any barrier
-  const int q0 = mt * BM, co0 = nt * BN;
+    const int q0 = mt * BM, co0 = nt * BN;
   const int nsteps = p.Cin / 32;
   const long long ldx6 = (long long)p.ldx * 3;
   const long long wslab = (long long)p.Cout * 48;  // one 16-deep chunk of the split codebook
@@ -2044,10 +2053,20 @@ __global__ void __launch_bounds__(512) vq_prefilter_x3(const ConvParams p) {
   };
   // nsteps is even (launcher): no odd exit, so the loop header never merges a path with this
   // step's loads still in flight (which made the waitcnt pass drain everything, vmcnt(0))
+#ifdef DCX_CLOCK_DIAG
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   for (int s = 0; s < nsteps; s += 2) {
     step(s, std::integral_constant<int, 0>{});
     step(s + 1, std::integral_constant<int, 1>{});
   }
+#ifdef DCX_CLOCK_DIAG
+  if (threadIdx.x == 0) {  // steps counted in units of 1536 ideal cycles (24 MFMAs x 2 waves per SIMD)
+    atomicAdd(&g_clock_diag[0], __builtin_amdgcn_s_memtime() - t0);
+    atomicAdd(&g_clock_diag[1], __builtin_amdgcn_s_memrealtime() - r0);
+    atomicAdd(&g_clock_diag[2], (unsigned long long)nsteps);
+  }
+#endif
   epilogue_top2<BM, BN, WM, WN>(p, acc, q0, co0, nt, ntiles, reinterpret_cast<float*>(lds));
 }
 
