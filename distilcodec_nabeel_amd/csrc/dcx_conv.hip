@@ -1862,23 +1862,16 @@ static bool x6dm_ok(const ConvParams& p, bool halo, int bn) {
   return (long long)(p.Lin + 1024) * arow < (1LL << 31) && 1024 * arow < (1LL << 31) && wbytes < (1LL << 31);
 }
 
-// Whether the 64K-output tiles of the LDS-DMA kernels (BM x bn) beat 256 x 128 tiles of
-// conv_gemm_x6pp / x6lm for this launch.  Both run one workgroup per CU, so a launch takes
-// ceil(tiles / CUs) rounds; the smaller tiles take half the time at ~0.88 of the rate (measured on
-// the generator and encoder shapes).  Few-tile launches (short clips, the streaming hop, K-heavy
-// 1x1 convs with narrow outputs) keep the smaller tiles for their parallelism.
-static bool big_tiles_pay(const ConvParams& p, int batch, int phases, int bn) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-      cus = 256;
-  }
+// Whether the 64K-output tiles of the LDS-DMA kernels (BM x bn) or the 256 x 128 tiles of
+// conv_gemm_x6pp / x6lm take a conv.  Both run one workgroup per CU; the smaller tiles take half the
+// time at ~0.88 of the rate, so they win when a launch has few tiles (the C5 streaming hop, short
+// clips, 1x1 convs with narrow outputs such as the encoder's 4C -> C).  The rule looks at one clip
+// (rows x column tiles x phases), never at the batch size: the two families sum in different
+// orders, and a clip must give the same bits alone as inside a batch of equal-length clips.
+// At C2's batch of 32 the threshold picks what ceil(tiles / CUs) rounds would.
+static bool big_tiles_pay(const ConvParams& p, int phases, int bn) {
   const int bm = 65536 / bn;
-  const long long big = (long long)((p.Lq + bm - 1) / bm) * (p.Cout / bn) * batch * phases;
-  const long long small = (long long)((p.Lq + 255) / 256) * (p.Cout / 128) * batch * phases;
-  const double cost_big = (double)((big + cus - 1) / cus), cost_small = (double)((small + cus - 1) / cus) * 0.5 / 0.88;
-  return cost_big <= cost_small;
+  return (long long)((p.Lq + bm - 1) / bm) * (p.Cout / bn) * phases >= 16;
 }
 
 template <int HALO, int BN>
@@ -2150,7 +2143,7 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       return launch_x6w8_af32<256, 32, 4, 1, 64>(p, batch, phases, s);
     }
 #ifndef DCX_NO_DM
-    if (!h && x6dm_ok(p, false, 256) && big_tiles_pay(p, batch, phases, 256))
+    if (!h && x6dm_ok(p, false, 256) && big_tiles_pay(p, phases, 256))
       return launch_x6dm<0, 256>(p, batch, phases, s, kname);  // x6 1-tap, Cout % 256
 #endif
 #ifndef DCX_NO_PP
@@ -2161,7 +2154,7 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       return launch_x6w8<128, 128, 2, 2, 0, false>(p, batch, phases, s);
     }
     if (p.Cout % 128 == 0) {
-      const bool pay256 = big_tiles_pay(p, batch, phases, 256), pay128 = big_tiles_pay(p, batch, phases, 128);
+      const bool pay256 = big_tiles_pay(p, phases, 256), pay128 = big_tiles_pay(p, phases, 128);
       (void)pay256;
       (void)pay128;
 #ifndef DCX_NO_DQ
