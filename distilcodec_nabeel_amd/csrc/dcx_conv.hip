@@ -1448,8 +1448,13 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6dm(const ConvParams p) {
   const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
   const int row0 = q0 + p.in_base[ph] + lo_rel;
   const int arow = p.ldx * 6;  // bytes per planes row
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.x6 + (long long)b * p.x_bstride * 3), 0, p.Lin * arow, 0x00020000);
+  // halo: descriptor over the clip (negative rows wrap past its range: zeros); 1-tap: over the
+  // tile's rows only, so clips of any length keep 32-bit offsets (row0 >= 0 without a halo)
+  const __amdgpu_buffer_rsrc_t rx =
+      HALO ? __builtin_amdgcn_make_buffer_rsrc((void*)(p.x6 + (long long)b * p.x_bstride * 3), 0, p.Lin * arow, 0x00020000)
+           : __builtin_amdgcn_make_buffer_rsrc((void*)(p.x6 + ((long long)b * p.x_bstride + (long long)row0 * p.ldx) * 3), 0,
+                                               max(0, min(BM, p.Lin - row0)) * arow, 0x00020000);
+  const int rbase = HALO ? row0 : 0;  // row of image row 0 relative to the descriptor
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.w6 + (long long)ph * taps * nchunks * p.Cout * 48), 0, taps * nchunks * p.Cout * 96, 0x00020000);
 
@@ -1462,7 +1467,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6dm(const ConvParams p) {
     const int P = (group * A_G + i * 4 + gw) * 64 + lane;
     const int row = P / 6, s = P - row * 6;
     const int hl = (s >= 3) ^ ((row >> 3) & 1), pl = s >= 3 ? s - 3 : s;
-    a_off[i] = (row0 + row) * arow + (hl * 3 + pl) * 16;  // negative rows: huge unsigned, out of range
+    a_off[i] = (rbase + row) * arow + (hl * 3 + pl) * 16;  // negative rows: huge unsigned, out of range
   }
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
@@ -1853,12 +1858,146 @@ static hipError_t launch_x6dq(const ConvParams& p, int batch, int phases, hipStr
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// conv_gemm_bf16dm: the DCX_GEMM_BF16 mode's 1x1 convs (one hi * hi' product, the reference's
+// enable_bfloat16 autocast) on the LDS-DMA ping-pong schedule of conv_gemm_x6dm.
+//
+// A step is K32 (two K16 chunks, hi planes only: 4 pieces of 16 B per row), 16x16x32 MFMAs on
+// 64 x 128 wave tiles: 32 MFMAs against 12 fragment reads per segment.  A and B ride one 3-slot
+// ring (step t in slot t % 3, 16 + 16 KiB per slot), issued by group 0 in MEM0(t - 3) and group 1
+// in MEM1(t - 2) and retired one memory segment later.  LDS images: 16-row blocks, piece-major
+// (16-byte unit (r >> 4) * 64 + piece * 16 + (r & 15), piece = 8-channel group of the step).
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
+  constexpr int BM = 256, BN = 256, WN = 2, WM = 4;
+  constexpr int WR = 64, WC = 128, TM = WR / 16, TN = WC / 16;
+  constexpr int A_G = BM * 4 / 128, B_G = BN * 4 / 128;  // DMA instructions per group per step
+  constexpr int A_PW = A_G / 4, B_PW = B_G / 4;
+  constexpr int ABUF = BM * 4 * 8, BBUF = BN * 4 * 8;    // ushorts
+  constexpr int LDS_US = 3 * (ABUF + BBUF);               // 96 KiB
+  __shared__ __attribute__((aligned(16))) unsigned short lds[LDS_US];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int group = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int wm = wave / WN, wn = wave % WN;
+  const int ntiles = p.Cout / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = wg / ntiles, nt = wg - mt * ntiles;
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int b = blockIdx.y, ph = blockIdx.z;
+  const int nsteps = p.Cin / 32;
+  const int arow = p.ldx * 6;
+  const int row0 = q0 + p.in_base[ph];  // >= 0 for 1x1 convs; the descriptor covers the tile's rows
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.x6 + ((long long)b * p.x_bstride + (long long)row0 * p.ldx) * 3), 0,
+      max(0, min(BM, p.Lin - row0)) * arow, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.w6 + (long long)ph * (p.Cin / 16) * p.Cout * 48), 0, (p.Cin / 16) * p.Cout * 96, 0x00020000);
+
+  // DMA pieces (bytes, step 0): unit u -> row (u / 64) * 16 + (u & 15), piece (u % 64) >> 4 = the
+  // 8-channel group kq; step s adds s * 192 (input) and s * Cout * 192 (weights: two K16 chunks)
+  int a_off[A_PW], b_off[B_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int u = (group * A_G + i * 4 + gw) * 64 + lane;
+    const int r = (u >> 6) * 16 + (u & 15), kq = (u & 63) >> 4;
+    a_off[i] = r * arow + kq * 48;  // rows past Lin: out of range, zeros
+  }
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int u = (group * B_G + i * 4 + gw) * 64 + lane;
+    const int c = (u >> 6) * 16 + (u & 15), kq = (u & 63) >> 4;
+    b_off[i] = (kq >> 1) * p.Cout * 96 + (co0 + c) * 96 + (kq & 1) * 48;
+  }
+  unsigned short* const a_dst = lds + (group * A_G + gw) * 512;
+  unsigned short* const b_dst = lds + 3 * ABUF + (group * B_G + gw) * 512;
+  auto dma_step = [&](int s, int slot) {
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) dma16(rx, a_dst + slot * ABUF + i * 2048, a_off[i] + s * 192, 0);
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) dma16(rw, b_dst + slot * BBUF + i * 2048, b_off[i], s * p.Cout * 192);
+    return A_PW + B_PW;
+  };
+
+  const int l15 = lane & 15, kq = lane >> 4;
+  const char* const ldsb = reinterpret_cast<const char*>(lds);
+  const int a_lane = (wm * WR / 16) * 1024 + kq * 256 + l15 * 16;           // bytes in an A image
+  const int b_lane = 6 * ABUF + (wn * WC / 16) * 1024 + kq * 256 + l15 * 16;  // bytes, B image of slot 0
+  s16x8 af[TM], bq[TN];
+  auto readF = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const s16x8*>(ldsb + slot * ABUF * 2 + a_lane + i * 1024);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bq[j] = *reinterpret_cast<const s16x8*>(ldsb + slot * BBUF * 2 + b_lane + j * 1024);
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                            __builtin_bit_cast(bf16x8, bq[j]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto inc3 = [](int& slot) { slot = slot == 2 ? 0 : slot + 1; };
+
+  for (int t = 0; t < 3; ++t)
+    if (t < nsteps) dma_step(t, t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  seg_barrier();
+  if (group == 0) {
+    readF(0);
+    int rs = 1, ws = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      mfma();  // MFMA(s)
+      seg_barrier();
+      if (s + 1 < nsteps) readF(rs);  // MEM0(s): fragments of step s + 1, issue step s + 3
+      int n = 0;
+      if (s + 3 < nsteps) n = dma_step(s + 3, ws);
+      wait_dma(n);
+      seg_barrier();
+      inc3(rs);
+      inc3(ws);
+    }
+  } else {
+    int rs = 0, ws = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      readF(rs);  // MEM1(s): fragments of step s, issue step s + 2 (s >= 1)
+      int n = 0;
+      if (s >= 1 && s + 2 < nsteps) n = dma_step(s + 2, ws);
+      wait_dma(n);
+      seg_barrier();
+      mfma();  // MFMA(s)
+      seg_barrier();
+      inc3(rs);
+      if (s >= 1) inc3(ws);
+      else ws = 0;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  epilogue_lds<BM, BN, WM, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+}
+
 // whether conv_gemm_x6dm takes the conv: planes input, Cout % 256, taps >= 2 with a halo or one
 // tap without, and 32-bit buffer offsets for the input rows (with the tile's halo) and the weights
+static bool in_base_nonneg(const ConvParams& p) {  // every phase's input row offset (unused entries are 0)
+  for (int i = 0; i < kMaxPhases; ++i)
+    if (p.in_base[i] < 0) return false;
+  return true;
+}
+
 static bool x6dm_ok(const ConvParams& p, bool halo, int bn) {
   if (!p.x6 || !p.w6 || p.nprod != 6 || p.Cout % bn || (halo ? p.taps < 2 : p.taps != 1)) return false;
   const long long arow = (long long)p.ldx * 6;
   const long long wbytes = (long long)p.taps * (p.Cin / BK) * p.Cout * 96;
+  if (!halo) return in_base_nonneg(p) && 1024 * arow < (1LL << 31) && wbytes < (1LL << 31);  // per-tile descriptor
   return (long long)(p.Lin + 1024) * arow < (1LL << 31) && 1024 * arow < (1LL << 31) && wbytes < (1LL << 31);
 }
 
@@ -2148,6 +2287,14 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
 #endif
 #ifndef DCX_NO_PP
     if (p.Cout % 128 == 0 && !h && !b1) return launch_x6pp<0>(p, batch, phases, s, kname);  // x6 1-tap
+#endif
+#ifndef DCX_NO_BF16DM
+    if (b1 && !h && p.taps == 1 && p.Cout % 256 == 0 && p.Cin % 32 == 0 && big_tiles_pay(p, phases, 256) &&
+        in_base_nonneg(p) && 1024LL * p.ldx * 6 < (1LL << 31) && (long long)(p.Cin / 16) * p.Cout * 96 < (1LL << 31)) {
+      if (kname) *kname = "conv_gemm_bf16dm<256,256>";
+      hipLaunchKernelGGL(conv_gemm_bf16dm, dim3(((p.Lq + 255) / 256) * (p.Cout / 256), batch, phases), dim3(512), 0, s, p);
+      return hipGetLastError();
+    }
 #endif
     if (p.Cout % 128 == 0 && !h) {  // 1-tap: 4-wave 128 x 128 tiles, two workgroups per CU
       name("conv_gemm_x6w4<128,128>", "conv_gemm_bf16w4<128,128>");

@@ -22,7 +22,8 @@ def _bf(t):
 
 
 @pytest.mark.parametrize("case", [(512, 512, 11, 5, 300), (1024, 4096, 1, 1, 190), (64, 64, 7, 3, 700),
-                                  (32, 32, 3, 1, 500), (128, 256, 7, 1, 93)], ids=lambda c: "x".join(map(str, c)))
+                                  (32, 32, 3, 1, 500), (128, 256, 7, 1, 93),
+                                  (256, 1024, 1, 1, 1100)], ids=lambda c: "x".join(map(str, c)))
 def test_conv_bf16(case):
     from distilcodec_nabeel_amd.engine import NativeConv
 
