@@ -1952,6 +1952,9 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
     if (t < nsteps) dma_step(t, t);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   seg_barrier();
+#ifdef DCX_CLOCK_DIAG
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (group == 0) {
     readF(0);
     int rs = 1, ws = 0;
@@ -1982,6 +1985,13 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef DCX_CLOCK_DIAG
+  if (threadIdx.x == 0) {  // steps counted in units of 1536 ideal cycles (a K32 step is 1024)
+    atomicAdd(&g_clock_diag[0], __builtin_amdgcn_s_memtime() - t0);
+    atomicAdd(&g_clock_diag[1], __builtin_amdgcn_s_memrealtime() - r0);
+    atomicAdd(&g_clock_diag[2], (unsigned long long)(nsteps * 2 / 3));
+  }
+#endif
   epilogue_lds<BM, BN, WM, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 

@@ -30,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--gemm", default="x6", choices=["x6", "bf16"])
     a = ap.parse_args()
     f = _native.lib().dcx_diag_clock
     f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
@@ -40,14 +41,14 @@ def main():
         conv = NativeConv(w, np.zeros(cout, np.float32), dilation=d)
         x = torch.randn(B, Lr, cin, device="cuda")
         for _ in range(5):
-            conv(x)
+            conv(x, gemm=a.gemm)
         torch.cuda.synchronize()
         out = (ctypes.c_ulonglong * 3)()
         f(out, 1)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.reps):
-            conv(x)
+            conv(x, gemm=a.gemm)
         e1.record()
         torch.cuda.synchronize()
         f(out, 1)
