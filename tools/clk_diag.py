@@ -23,7 +23,8 @@ from distilcodec_nabeel_amd.engine import NativeConv  # noqa: E402
 T = 937
 SHAPES = {"res512_k3": (512, 512, 3, 1, 32, 8 * T), "res512_k11d5": (512, 512, 11, 5, 32, 8 * T),
           "res256_k7d3": (256, 256, 7, 3, 32, 32 * T), "pw_1024": (1024, 4096, 1, 1, 1, 32 * T),
-          "res64_k7d3": (64, 64, 7, 3, 32, 128 * T), "res64_k3d1": (64, 64, 3, 1, 32, 128 * T)}
+          "res64_k7d3": (64, 64, 7, 3, 32, 128 * T), "res64_k3d1": (64, 64, 3, 1, 32, 128 * T),
+          "res128_k11": (128, 128, 11, 1, 32, 64 * T), "res128_k3": (128, 128, 3, 1, 32, 64 * T)}
 
 
 def main():

@@ -17,6 +17,7 @@ SHAPES = {  # name: (cin, cout, k, dil, transposed, stride, B, L)
     "res512_k11d5": (512, 512, 11, 5, False, 1, 32, 8 * T),
     "res256_k7d3": (256, 256, 7, 3, False, 1, 32, 32 * T),
     "res128_k11": (128, 128, 11, 1, False, 1, 32, 64 * T),
+    "res128_k3": (128, 128, 3, 1, False, 1, 32, 64 * T),
     "res64_k7d3": (64, 64, 7, 3, False, 1, 32, 128 * T),
     "res32_k11d5": (32, 32, 11, 5, False, 1, 32, 256 * T),
     "res32_k7d3": (32, 32, 7, 3, False, 1, 32, 256 * T),
