@@ -137,6 +137,12 @@ int fail(dcx_codec* h, int code, const std::string& m) {
       return fail(h, DCX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
   } while (0)
 
+#define RUN(expr)             \
+  do {                        \
+    int rc_ = (expr);         \
+    if (rc_ != DCX_OK) return rc_; \
+  } while (0)
+
 // ----------------------------------------------------------------------------------------
 // profiling
 // ----------------------------------------------------------------------------------------
@@ -512,13 +518,13 @@ struct ConvCall {
 // staging; conv_gemm_x6w8 AF32).
 bool f32_input_ok(const ConvW& w) { return w.cin <= 128 && w.cout <= 64 && w.taps >= 2; }
 
-int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, bool force_f32 = false) {
+int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32, ConvParams& p) {
   const bool x6 = x6_mode(h) && !force_f32;
   const bool x6_f32in = x6 && !c.x.p && c.x.f && f32_input_ok(w);
   if (c.silu_in && !x6_f32in) return fail(h, DCX_ERR_STATE, "internal: silu_in needs an fp32-input conv");
   if (x6 ? ((!c.x.p && !x6_f32in) || !w.w6) : !c.x.f)
     return fail(h, DCX_ERR_STATE, "internal: conv input missing for GEMM mode");
-  ConvParams p{};
+  p = ConvParams{};
   p.x = c.x.f;
   p.x6 = x6 ? c.x.p : nullptr;
   p.w = w.w;
@@ -550,12 +556,49 @@ int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, boo
   p.nprod = one ? 1 : 6;
   p.round_bf16 = one;
   p.silu_in = c.silu_in;
+  return DCX_OK;
+}
+
+// algorithmic FLOPs and bytes of one conv (profiling)
+double conv_flops(const ConvW& w, const ConvCall& c) { return 2.0 * c.batch * c.Lq * w.phases * w.cout * w.cin * w.taps; }
+double conv_bytes(const ConvW& w, const ConvCall& c) {
+  const double outs = (double)c.batch * c.Lq * w.phases * w.cout;
+  return 4.0 * ((double)c.batch * c.Lin * w.cin + outs + (double)w.phases * w.cout * w.taps * w.cin);
+}
+
+int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, bool force_f32 = false) {
+  ConvParams p;
+  RUN(conv_params(h, w, c, force_f32, p));
   ProfScope ps(h, s);
   const char* kname = "conv";
   HIPCHK(h, dcx::launch_conv(p, c.batch, w.phases, s, &kname));
-  const double outs = (double)c.batch * c.Lq * w.phases * w.cout;
-  ps.done(kname, 2.0 * outs * w.cin * w.taps,
-          4.0 * ((double)c.batch * c.Lin * w.cin + outs + (double)w.phases * w.cout * w.taps * w.cin));
+  ps.done(kname, conv_flops(w, c), conv_bytes(w, c));
+  return DCX_OK;
+}
+
+// n independent convs (same batch) as one grouped launch when the kernel family allows it
+// (dcx::launch_conv_group), otherwise one by one; the results are the same bits either way.
+int run_conv_group(dcx_codec* h, const ConvW* const* w, const ConvCall* c, int n, hipStream_t s) {
+  ConvParams p[dcx::kMaxGroup];
+  double fl = 0, by = 0;
+  bool same = true;
+  for (int i = 0; i < n; ++i) {
+    RUN(conv_params(h, *w[i], c[i], false, p[i]));
+    fl += conv_flops(*w[i], c[i]);
+    by += conv_bytes(*w[i], c[i]);
+    same = same && c[i].batch == c[0].batch && w[i]->phases == 1;
+  }
+  if (same && n > 1) {
+    ProfScope ps(h, s);
+    const char* kname = "conv_group";
+    const hipError_t e = dcx::launch_conv_group(p, n, c[0].batch, s, &kname);
+    if (e == hipSuccess) {
+      ps.done(kname, fl, by);
+      return DCX_OK;
+    }
+    if (e != hipErrorNotSupported) HIPCHK(h, e);
+  }
+  for (int i = 0; i < n; ++i) RUN(run_conv(h, *w[i], c[i], s));
   return DCX_OK;
 }
 
@@ -579,11 +622,6 @@ ConvCall framed(CAct x, int B, int L, int C) {
   return c;
 }
 
-#define RUN(expr)             \
-  do {                        \
-    int rc_ = (expr);         \
-    if (rc_ != DCX_OK) return rc_; \
-  } while (0)
 
 #define LAUNCH(h, s, name, flops, bytes, expr) \
   do {                                         \
@@ -783,13 +821,21 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
   const dcx_config& c = h->cfg;
   RUN(ensure_planes(h, z, (long long)B * T, c.vq_dim, ws, s));
   const size_t per = (size_t)B * T * max_gen_width(c);
+  // The ParallelBlock's ResBlocks are independent until the mean, so each keeps its own state and
+  // the convs of one dilation index run as one grouped launch (run_conv_group).
+  constexpr int NR = dcx::kMaxGroup;
+  if (c.n_res > NR) return fail(h, DCX_ERR_INVALID_ARG, "more ResBlocks per stage than supported");
   float* X = ws.f(per);   // ConvT output (residual of each ResBlock's first pair)
-  float* R = ws.f(per);   // ResBlock state
   float* Mx = ws.f(per);  // ParallelBlock mean accumulator; silu(mean) of the last stage
   Act S = conv_input(h, ws, per);   // silu(stage input) -> ConvT
   Act XS = conv_input(h, ws, per);  // silu(X)
-  Act RS = conv_input(h, ws, per);  // silu(R)
-  Act Tb = conv_input(h, ws, per);  // silu(c1 output)
+  float* R[NR];                     // ResBlock states
+  Act RS[NR], Tb[NR];               // silu(R), silu(c1 output)
+  for (int rb = 0; rb < c.n_res; ++rb) {
+    R[rb] = ws.f(per);
+    RS[rb] = conv_input(h, ws, per);
+    Tb[rb] = conv_input(h, ws, per);
+  }
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for generate");
   // Tensors consumed by small-Cout convs are kept in fp32 (those kernels split them while
@@ -808,7 +854,12 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
     const ConvW& up = h->ups[i];
     const int Co = up.cout, Lo = L * c.up_rates[i];
     const ConvW& rconv = h->res[i][0][0][0];  // every ResBlock conv of the stage has Cin = Cout = Co
-    const Act S_i = in_form(S, up), XS_i = in_form(XS, rconv), RS_i = in_form(RS, rconv), Tb_i = in_form(Tb, rconv);
+    const Act S_i = in_form(S, up), XS_i = in_form(XS, rconv);
+    Act RS_i[NR], Tb_i[NR];
+    for (int rb = 0; rb < c.n_res; ++rb) {
+      RS_i[rb] = in_form(RS[rb], rconv);
+      Tb_i[rb] = in_form(Tb[rb], rconv);
+    }
     // fp32-input stages: the first conv of each pair applies silu to X / R while staging, so
     // silu(X) and silu(R) are never written (7 activation tensors per stage less HBM traffic)
     const bool silu_on_load = x6_mode(h) && f32_input_ok(rconv);
@@ -819,23 +870,34 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
       RUN(run_conv(h, up, cc, s));
     }
     const bool last_stage = i == c.n_ups - 1;
-    for (int rb = 0; rb < c.n_res; ++rb) {
-      for (int ci = 0; ci < 3; ++ci) {
-        const Act& src = silu_on_load ? Act{ci == 0 ? X : R, nullptr} : (ci == 0 ? XS_i : RS_i);
-        const float* resid = ci == 0 ? X : R;
-        {
-          ConvCall cc = framed(src, B, Lo, Co);
-          cc.silu_in = silu_on_load;
-          cc.silu_to(Tb_i);
-          RUN(run_conv(h, h->res[i][rb][ci][0], cc, s));
+    for (int ci = 0; ci < 3; ++ci) {
+      const ConvW* w1[NR];
+      ConvCall c1[NR];
+      for (int rb = 0; rb < c.n_res; ++rb) {  // c1 of every ResBlock: one grouped launch
+        const Act src = silu_on_load ? Act{ci == 0 ? X : R[rb], nullptr} : (ci == 0 ? XS_i : RS_i[rb]);
+        c1[rb] = framed(src, B, Lo, Co);
+        c1[rb].silu_in = silu_on_load;
+        c1[rb].silu_to(Tb_i[rb]);
+        w1[rb] = &h->res[i][rb][ci][0];
+      }
+      RUN(run_conv_group(h, w1, c1, c.n_res, s));
+      if (ci < 2) {  // c2 of every ResBlock: grouped; residual X (first pair) or the block's state
+        const ConvW* w2[NR];
+        ConvCall c2[NR];
+        for (int rb = 0; rb < c.n_res; ++rb) {
+          c2[rb] = framed(Tb_i[rb], B, Lo, Co);
+          c2[rb].epi = dcx::EPI_RES;
+          c2[rb].res = ci == 0 ? X : R[rb];
+          c2[rb].y = R[rb];
+          if (!silu_on_load) c2[rb].silu_to(RS_i[rb]);
+          w2[rb] = &h->res[i][rb][ci][1];
         }
-        ConvCall cc = framed(Tb_i, B, Lo, Co);
-        cc.epi = dcx::EPI_RES;
-        cc.res = resid;
-        if (ci < 2) {
-          cc.y = R;
-          if (!silu_on_load) cc.silu_to(RS_i);
-        } else {
+        RUN(run_conv_group(h, w2, c2, c.n_res, s));
+      } else {  // last pair: ParallelBlock mean folded into the epilogues, in ResBlock order
+        for (int rb = 0; rb < c.n_res; ++rb) {
+          ConvCall cc = framed(Tb_i[rb], B, Lo, Co);
+          cc.epi = dcx::EPI_RES;
+          cc.res = R[rb];
           cc.macc = Mx;
           cc.mean = rb == 0 ? dcx::MEAN_FIRST : (rb == c.n_res - 1 ? dcx::MEAN_LAST : dcx::MEAN_MID);
           if (rb == c.n_res - 1) {
@@ -843,8 +905,8 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
             if (last_stage) cc.y2 = Mx;
             else cc.silu_to(in_form(S, h->ups[i + 1]));  // input of the next ConvT
           }
+          RUN(run_conv(h, h->res[i][rb][ci][1], cc, s));
         }
-        RUN(run_conv(h, h->res[i][rb][ci][1], cc, s));
       }
     }
     C = Co;

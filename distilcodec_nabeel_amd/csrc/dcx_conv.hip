@@ -1631,8 +1631,9 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6dm(const ConvParams p) {
 // (r & 15) for piece s = half * 3 + plane of row r; every ds_read_b128 then touches 16
 // consecutive rows of one piece per lane group (conflict-free at any tap offset).
 // ---------------------------------------------------------------------------------------------
+// One output tile (wg = row tile * column tiles + column tile, clip b, phase ph).
 template <int BN>
-__global__ void __launch_bounds__(512, 2) conv_gemm_x6dq(const ConvParams p) {
+__device__ __forceinline__ void x6dq_tile(const ConvParams& p, const int wg, const int b, const int ph) {
   constexpr int HALO = 64;
   constexpr int BM = 65536 / BN, WN = 2;
   constexpr int WR = BM / 4, WC = BN / 2, TM = WR / 16, TN = WC / 16;
@@ -1651,10 +1652,8 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6dq(const ConvParams p) {
   const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
   const int wm = wave >> 1, wn = wave & 1;
   const int ntiles = p.Cout / BN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
-  const int b = blockIdx.y, ph = blockIdx.z;
   const int nchunks = p.Cin / BK;
   const int taps = p.taps;
   const int nsteps = nchunks * taps;
@@ -1847,6 +1846,31 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6dq(const ConvParams p) {
   }
 #endif
   epilogue_lds<BM, BN, 4, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+}
+
+template <int BN>
+__global__ void __launch_bounds__(512, 2) conv_gemm_x6dq(const ConvParams p) {
+  x6dq_tile<BN>(p, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y, blockIdx.z);
+}
+
+// Grouped launch: up to 3 independent convs with the same tiling (the three ResBlocks' convs of one
+// dilation index, tap counts 3 / 7 / 11), longest first, so the short ones fill the last round.
+template <int BN>
+__global__ void __launch_bounds__(512, 2) conv_gemm_x6dq_group(const ConvGroup g) {
+  // member by raw block index, so every XCD (block index mod 8) gets its share of each member's
+  // tiles; a remap of the whole grid would hand the 11-tap tiles to the first XCDs and the 3-tap
+  // ones to the last
+  const int t = blockIdx.x;
+  const int k = t >= g.start[1] ? (t >= g.start[2] ? 2 : 1) : 0;
+  const int local = xcd_remap(t - g.start[k], g.start[k + 1] - g.start[k]);
+  const int b = local / g.tiles_per_clip[k];
+  // a private copy: the tile body's inline-asm barriers clobber memory, which would make the
+  // compiler re-read every field of a kernarg-resident struct after each of them
+  ConvParams p;
+  if (k == 0) p = g.p[0];
+  else if (k == 1) p = g.p[1];
+  else p = g.p[2];
+  x6dq_tile<BN>(p, local - b * g.tiles_per_clip[k], b, 0);
 }
 
 template <int BN>
@@ -2354,6 +2378,43 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
   }
   if (kname) *kname = "conv_gemm_f32<256,32>";
   return launch_f32<256, 32, 4, 1, false>(p, batch, phases, s);
+}
+
+hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t s, const char** kname) {
+  if (n < 1 || n > kMaxGroup || batch < 1) return hipErrorInvalidValue;
+  const int cout = ps[0].Cout;
+  const int bn = cout % 256 == 0 ? 256 : 128, bm = 65536 / bn;
+  // every member must be one launch_conv would give to conv_gemm_x6dq<bn> (same bits either way)
+  for (int i = 0; i < n; ++i) {
+    const ConvParams& p = ps[i];
+    if (p.Cout != cout || cout % 128 || p.Cin % BK || !p.x6 || !p.w6 || p.nprod != 6 || p.taps < 3 ||
+        tap_span(p) == 0 || tap_span(p) > 64 || (p.Cin / BK) * p.taps % 2 || !x6dm_ok(p, true, bn) ||
+        !big_tiles_pay(p, 1, bn))
+      return hipErrorNotSupported;
+  }
+  int order[kMaxGroup] = {0, 1, 2};  // longest (most taps) first
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j)
+      if (ps[order[j]].taps > ps[order[i]].taps) std::swap(order[i], order[j]);
+  ConvGroup g{};
+  long long start = 0;
+  for (int k = 0; k < n; ++k) {
+    const ConvParams& p = ps[order[k]];
+    g.p[k] = p;
+    g.tiles_per_clip[k] = ((p.Lq + bm - 1) / bm) * (cout / bn);
+    g.start[k] = (int)start;
+    start += (long long)g.tiles_per_clip[k] * batch;
+  }
+  if (start > (1LL << 30)) return hipErrorInvalidValue;
+  for (int k = n; k <= kMaxGroup; ++k) g.start[k] = (int)start;
+  if (bn == 256) {
+    if (kname) *kname = "conv_gemm_x6dq_group<256,256,halo>";
+    hipLaunchKernelGGL((conv_gemm_x6dq_group<256>), dim3((unsigned)start), dim3(512), 0, s, g);
+  } else {
+    if (kname) *kname = "conv_gemm_x6dq_group<512,128,halo>";
+    hipLaunchKernelGGL((conv_gemm_x6dq_group<128>), dim3((unsigned)start), dim3(512), 0, s, g);
+  }
+  return hipGetLastError();
 }
 
 int vq_argmin_ntiles(int ncodes) { return ncodes / 128; }

@@ -61,8 +61,21 @@ struct ConvParams {
   int silu_in;
 };
 
+// Independent convs issued as one launch (launch_conv_group); problem k owns logical tiles
+// [start[k], start[k + 1]), tiles_per_clip[k] per clip.
+constexpr int kMaxGroup = 3;
+struct ConvGroup {
+  ConvParams p[kMaxGroup];
+  int start[kMaxGroup + 1];
+  int tiles_per_clip[kMaxGroup];
+};
+
 // Launchers (all stream-ordered, no allocation).  Return hipError_t of the launch.
 hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname);
+// n <= kMaxGroup independent single-phase convs with one column tiling as one launch of the
+// LDS-DMA 16x16x32 kernel; hipErrorNotSupported when they do not all qualify (the caller then
+// launches them one by one, which gives the same bits).
+hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t s, const char** kname);
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname);
 int vq_argmin_ntiles(int ncodes);
 // VQ search, x6 mode: bf16x3 prefilter (approximate squared distances, per-tile top 2) ...

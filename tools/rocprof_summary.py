@@ -33,6 +33,8 @@ def short(name):
         return f"{base}<{bm},{bn},halo>" if parts[0] != "0" else f"{base}<{bm},{bn}>"
     if base == "conv_gemm_bf16dm":
         return "conv_gemm_bf16dm<256,256>"
+    if base == "conv_gemm_x6dq_group":  # <BN>, halo
+        return f"{base}<{65536 // int(parts[0])},{parts[0]},halo>"
     if base == "conv_gemm_x6dq":  # <BN>, halo
         return f"{base}<{65536 // int(parts[0])},{parts[0]},halo>"
     if base == "vq_prefilter_x3":
