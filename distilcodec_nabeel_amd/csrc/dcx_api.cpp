@@ -730,8 +730,8 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   const dcx_config& c = h->cfg;
   const long long M = (long long)B * T;
   const int D = c.vq_dim, CD = c.codebook_dim, NC = c.codebook_size;
-  const int ntiles = dcx::vq_argmin_ntiles(NC);
   const bool x6 = x6_mode(h);
+  const int ntiles = x6 ? dcx::vq_prefilter_ntiles(NC, CD) : dcx::vq_argmin_ntiles(NC);
   RUN(ensure_planes(h, feat, M, D, ws, s));
   float* X = ws.f((size_t)M * D);
   unsigned short* X6 = x6 ? ws.u16((size_t)M * D * 3) : nullptr;

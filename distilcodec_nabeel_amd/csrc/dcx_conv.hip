@@ -2237,6 +2237,168 @@ __global__ void __launch_bounds__(512) vq_prefilter_x3(const ConvParams p) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// vq_prefilter_dm: the VQ prefilter on the conv_gemm_x6dm schedule.
+//
+// vq_prefilter_x3 issues its MFMAs about half of the time: with 64 x 64 wave tiles its LDS traffic
+// (16 fragment reads and 6 register-staged stores per 24 MFMAs) is close to the LDS bandwidth, and
+// moving it to LDS-DMA alone did not help.  Here the tiles are 256 x 256 with 64 x 128 wave tiles
+// (12 fragment reads per 24 MFMAs, no ds_write pass), staged by LDS-DMA into a 3-slot ring and
+// run on the two-group ping-pong schedule of conv_gemm_x6dm (1-tap: every K16 step brings its own
+// input and codebook tiles).  Each input row panel is also re-read by half as many code tiles.
+// The products per K16 (m*h', h*m', h*h', in that order, on 32x32x16) and so the error bound of
+// launch_vq_prefilter are those of vq_prefilter_x3.
+// LDS images: 64-byte rows holding the hi and mid pieces of both K halves (piece = half * 2 +
+// plane) in slot piece ^ ((row >> 2) & 3), which keeps every 16-lane group of a b128 fragment read
+// on 64 distinct banks; lane-linear per DMA instruction, the swizzle applied on the source.
+// Rows past the input end are outside the (per-tile) buffer descriptor and load zeros.
+// XMID = false (bf16 mode, mid plane of x zero): the m*h' MFMA is skipped.
+// ---------------------------------------------------------------------------------------------
+template <bool XMID>
+__global__ void __launch_bounds__(512, 2) vq_prefilter_dm(const ConvParams p) {
+  constexpr int BM = 256, BN = 256, WN = 2;
+  constexpr int WR = BM / 4, WC = BN / 2, TM = WR / 32, TN = WC / 32;
+  constexpr int RW = 32;                          // ushorts per LDS row
+  constexpr int G_I = BM * 4 / 64 / 2;            // DMA instructions per group per tile (A or B)
+  constexpr int PW = G_I / 4;                     // ... per wave
+  constexpr int ABUF = BM * RW, BBUF = BN * RW;
+  constexpr int LDS_US = 3 * ABUF + 3 * BBUF;
+  static_assert(BM == BN && G_I % 4 == 0 && LDS_US * 2 <= 160 * 1024, "tile shape");
+  __shared__ __attribute__((aligned(16))) unsigned short lds[LDS_US];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int group = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int wm = wave >> 1, wn = wave & 1;
+  // grouped order (as vq_prefilter_x3): 16 row panels x 16 code tiles resident together, 4 x 8 per
+  // XCD, so the blocks of one XCD stream the same panels through its L2 (ntiles % 16 == 0)
+  const int ntiles = p.Cout / BN, mtiles = (p.Lq + BM - 1) / BM;
+  const int bid = blockIdx.x, xc = bid & 7, l = (bid >> 3) & 31, sup = bid >> 8;
+  const int nsm = (mtiles + 15) >> 4;
+  const int mt = (sup % nsm) * 16 + (xc & 3) * 4 + (l & 3);
+  const int nt = (sup / nsm) * 16 + (xc >> 2) * 8 + (l >> 2);
+  if (mt >= mtiles) return;  // whole workgroup, before any barrier
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int nsteps = p.Cin / BK;
+  const int arow = p.ldx * 6;  // bytes per planes row
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.x6 + (long long)q0 * p.ldx * 3), 0, min(BM, p.Lq - q0) * arow, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.w6, 0, nsteps * p.Cout * 96, 0x00020000);
+
+  int a_off[PW], b_off[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int u = (group * G_I + i * 4 + gw) * 64 + lane;
+    const int row = u >> 2, pc = (u & 3) ^ ((row >> 2) & 3);
+    const int poff = (pc >> 1) * 48 + (pc & 1) * 16;  // (half, plane) within a 96-byte K16 chunk
+    a_off[i] = row * arow + poff;
+    b_off[i] = (co0 + row) * 96 + poff;
+  }
+  unsigned short* const a_dst = lds + (group * G_I + gw) * 512;
+  unsigned short* const b_dst = lds + 3 * ABUF + (group * G_I + gw) * 512;
+  auto dma_step = [&](int c, int slot) {
+#pragma unroll
+    for (int i = 0; i < PW; ++i) dma16(rx, a_dst + slot * ABUF + i * 2048, a_off[i] + c * 96, 0);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) dma16(rw, b_dst + slot * BBUF + i * 2048, b_off[i], c * p.Cout * 96);
+    return 2 * PW;
+  };
+
+  const int lrow = lane & 31, h = lane >> 5;
+  s16x8 af[TM][2], bfr[TN][2];
+  auto readF = [&](int slot) {
+    const unsigned short* A = lds + slot * ABUF;
+    const unsigned short* Bs = lds + 3 * ABUF + slot * BBUF;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm * WR + i * 32 + lrow;
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl)
+        af[i][pl] = *reinterpret_cast<const s16x8*>(A + r * RW + (((h * 2 + pl) ^ ((r >> 2) & 3)) << 3));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WC + j * 32 + lrow;
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl)
+        bfr[j][pl] = *reinterpret_cast<const s16x8*>(Bs + col * RW + (((h * 2 + pl) ^ ((col >> 2) & 3)) << 3));
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  auto mfma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (XMID)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[i][1]),
+                                                              __builtin_bit_cast(bf16x8, bfr[j][0]), acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[i][0]),
+                                                            __builtin_bit_cast(bf16x8, bfr[j][1]), acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[i][0]),
+                                                            __builtin_bit_cast(bf16x8, bfr[j][0]), acc[i][j], 0, 0, 0);
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto inc3 = [](int& slot) { slot = slot == 2 ? 0 : slot + 1; };
+
+  // ---- prologue: steps 0, 1, 2 (both groups their pieces), drained
+  for (int t = 0; t < 3; ++t) dma_step(t, t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  seg_barrier();
+#ifdef DCX_CLOCK_DIAG
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  // Segment 2s: group 0 MFMA(s), group 1 MEM1(s); 2s + 1: group 0 MEM0(s), group 1 MFMA(s).
+  if (group == 0) {
+    readF(0);
+    int rs = 1, ws = 0;  // slot of step s + 1 (read next), of step s + 3 (issued next)
+    for (int s = 0; s < nsteps; ++s) {
+      mfma();  // MFMA(s)
+      seg_barrier();
+      // MEM0(s): fragments of step s + 1, issue step s + 3, retire step s + 2
+      if (s + 1 < nsteps) readF(rs);
+      int n = 0;
+      if (s + 3 < nsteps) n = dma_step(s + 3, ws);
+      wait_dma(n);
+      seg_barrier();
+      inc3(rs);
+      inc3(ws);
+    }
+  } else {
+    int rs = 0, ws = 0;  // slot of step s, of step s + 2
+    for (int s = 0; s < nsteps; ++s) {
+      // MEM1(s): fragments of step s, issue step s + 2 (s >= 1), retire step s + 1
+      readF(rs);
+      int n = 0;
+      if (s >= 1 && s + 2 < nsteps) n = dma_step(s + 2, ws);
+      wait_dma(n);
+      seg_barrier();
+      mfma();  // MFMA(s)
+      seg_barrier();
+      inc3(rs);
+      if (s >= 1) inc3(ws);
+      else ws = 0;  // step 3's slot
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef DCX_CLOCK_DIAG
+  if (threadIdx.x == 0) {  // steps counted in units of vq_prefilter_x3's (K32: twice these)
+    atomicAdd(&g_clock_diag[0], __builtin_amdgcn_s_memtime() - t0);
+    atomicAdd(&g_clock_diag[1], __builtin_amdgcn_s_memrealtime() - r0);
+    atomicAdd(&g_clock_diag[2], (unsigned long long)nsteps / 2);
+  }
+#endif
+  epilogue_top2<BM, BN, 4, WN>(p, acc, q0, co0, nt, ntiles, reinterpret_cast<float*>(lds));
+}
+
+// ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, bool ARGMIN>
@@ -2419,6 +2581,16 @@ hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t
 
 int vq_argmin_ntiles(int ncodes) { return ncodes / 128; }
 
+// code tile of the x6-mode prefilter: 256 (vq_prefilter_dm) where its shape limits hold, else 128
+static bool vq_dm_ok(int ncodes, int dim) {
+#ifdef DCX_NO_VQDM
+  return false;
+#endif
+  return ncodes % (256 * 16) == 0 && dim % BK == 0 && dim / BK >= 3 && (long long)dim * 6 * 256 < (1ll << 31) &&
+         (long long)(dim / BK) * ncodes * 96 < (1ll << 31);
+}
+int vq_prefilter_ntiles(int ncodes, int dim) { return ncodes / (vq_dm_ok(ncodes, dim) ? 256 : 128); }
+
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname) {
   if (p.Cin % BK || p.Cout % 128) return hipErrorInvalidValue;
   ConvParams q = p;
@@ -2442,6 +2614,14 @@ hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipSt
   q.Lq = rows;
   q.Lin = rows;
   q.taps = 1;
+  if (vq_dm_ok(p.Cout, p.Cin)) {
+    const int mtiles = (rows + 255) / 256, ntiles = p.Cout / 256;
+    const dim3 grid((unsigned)(((mtiles + 15) / 16) * (ntiles / 16) * 256));
+    if (kname) *kname = x_bf16 ? "vq_prefilter_dm_x2<256,256>" : "vq_prefilter_dm<256,256>";
+    if (x_bf16) hipLaunchKernelGGL((vq_prefilter_dm<false>), grid, dim3(512), 0, s, q);
+    else hipLaunchKernelGGL((vq_prefilter_dm<true>), grid, dim3(512), 0, s, q);
+    return hipGetLastError();
+  }
   const int mtiles = (rows + BM - 1) / BM, ntiles = p.Cout / BN;
   const int nsm = (mtiles + 15) / 16;
   dim3 grid((unsigned)(nsm * (ntiles / 16) * 256));

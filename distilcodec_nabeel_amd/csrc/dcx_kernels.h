@@ -78,6 +78,8 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
 hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t s, const char** kname);
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname);
 int vq_argmin_ntiles(int ncodes);
+// per-row partial count of the x6-mode prefilter (launch_vq_prefilter)
+int vq_prefilter_ntiles(int ncodes, int dim);
 // VQ search, x6 mode: bf16x3 prefilter (approximate squared distances, per-tile top 2) ...
 // x_bf16: the rows of x are bf16 values (mid and lo planes zero), which drops the mid*hi product.
 hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipStream_t s, const char** kname);

@@ -37,6 +37,8 @@ def short(name):
         return f"{base}<{65536 // int(parts[0])},{parts[0]},halo>"
     if base == "conv_gemm_x6dq":  # <BN>, halo
         return f"{base}<{65536 // int(parts[0])},{parts[0]},halo>"
+    if base == "vq_prefilter_dm":  # <XMID>
+        return "vq_prefilter_dm<256,256>" if parts and parts[0] == "true" else "vq_prefilter_dm_x2<256,256>"
     if base == "vq_prefilter_x3":
         kind = "vq_prefilter_x3" if len(parts) < 5 or parts[4] == "true" else "vq_prefilter_x2"
         return f"{kind}<{parts[0]},{parts[1]}>"
