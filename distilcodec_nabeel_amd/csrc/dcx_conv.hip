@@ -143,8 +143,8 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
 #ifdef DCX_DIAG_NOEPI
   if (q0 >= 0) return;  // timing-only build: main loop without the epilogue
 #endif
-#pragma unroll 1
-  for (int r0 = 0; r0 < BM; r0 += RPP) {
+  // acc rows [r0, r0 + RPP) of the tile -> LDS
+  auto stage_acc = [&](int r0) {
     __syncthreads();
     if (wm * WR >= r0 && wm * WR < r0 + RPP) {
       if constexpr (M16) {  // 16x16 block: lane holds column l & 15, rows 4 (l >> 4) + e
@@ -170,67 +170,88 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
       }
     }
     __syncthreads();
-    // Each thread always finishes the same 4 output channels (NT is a multiple of BN / 4), so
-    // bias and gamma are loaded once per tile, and the residual / mean-accumulator loads of IB
-    // rows are issued before their stores: the stores may alias them (the in-place ResBlock
-    // state), so hipcc would otherwise wait for one memory round trip per row.
-    constexpr int RSTEP = NT / (BN / 4), ROWS_T = RPP / RSTEP, IB = ROWS_T < 4 ? ROWS_T : 4;
-    static_assert(RPP % RSTEP == 0 && ROWS_T % IB == 0, "epilogue rows per thread");
+  };
+  // Each thread always finishes the same 4 output channels (NT is a multiple of BN / 4), so bias
+  // and gamma are loaded once per tile.  The residual / mean-accumulator rows of a batch are all
+  // loaded (unconditionally, past-the-end rows clamped) before any of its stores, and the first
+  // batch of a pass before the pass's LDS staging: with stores in flight hipcc can only wait with
+  // vmcnt(0), and conditional loads in a rolled loop made it wait before every single load (one
+  // memory round trip per row).  The stores may alias the loads (the in-place ResBlock state);
+  // each thread stores only elements it has already loaded.
+  constexpr int RSTEP = NT / (BN / 4), ROWS_T = RPP / RSTEP;
+  static_assert(RPP % RSTEP == 0, "epilogue rows per thread");
+  const bool need_r = p.epi == EPI_GAMMA_RES || p.epi == EPI_RES;
+  const bool need_m = p.mean_mode == MEAN_MID || p.mean_mode == MEAN_LAST;
+  auto batch = [&](int r0, int rb, bool stage, auto ibt) {
+    constexpr int IB = decltype(ibt)::value;
+    f32x4 r[IB], m[IB];
+    auto lofs = [&](int k) {
+      const int q = min(q0 + r0 + trow + (rb + k) * RSTEP, p.Lq - 1);
+      return ob + ((long long)q * p.out_mul + ph) * p.ldy + co;
+    };
+    if (need_r) {
+#pragma unroll
+      for (int k = 0; k < IB; ++k) r[k] = *reinterpret_cast<const f32x4*>(p.res + lofs(k));
+    }
+    if (need_m) {
+#pragma unroll
+      for (int k = 0; k < IB; ++k) m[k] = *reinterpret_cast<const f32x4*>(p.macc + lofs(k));
+    }
+    if (stage) stage_acc(r0);
+#pragma unroll
+    for (int k = 0; k < IB; ++k) {
+      const int rl = trow + (rb + k) * RSTEP;
+      const int q = q0 + r0 + rl;
+      if (q >= p.Lq) continue;
+      const long long orow = (long long)q * p.out_mul + ph;
+      const long long o = ob + orow * p.ldy + co;
+      f32x4 x = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + c4) + bias4;
+      if (p.round_bf16) x = round_bf16x4(x);
+      switch (p.epi) {
+        case EPI_GELU:
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = gelu_f(x[e]);
+          if (p.round_bf16) x = round_bf16x4(x);
+          break;
+        case EPI_GAMMA_RES: x = r[k] + gamma4 * x; break;
+        case EPI_RES: x = r[k] + x; break;
+        case EPI_LOGCLAMP:
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = logf(fmaxf(x[e], 1e-5f));
+          break;
+        default: break;
+      }
+      if (p.mean_mode == MEAN_FIRST) {
+        *reinterpret_cast<f32x4*>(p.macc + o) = x;
+        continue;
+      } else if (p.mean_mode == MEAN_MID) {
+        *reinterpret_cast<f32x4*>(p.macc + o) = m[k] + x;
+        continue;
+      } else if (p.mean_mode == MEAN_LAST) {
+        x = (m[k] + x) / 3.0f;
+      }
+      if (p.y) *reinterpret_cast<f32x4*>(p.y + o) = x;
+      if (y6) store_planes4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
+      if (p.y2 || y6s) {
+        f32x4 sv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sv[e] = silu_f(x[e]);
+        if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
+        if (y6s) store_planes4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+      }
+    }
+  };
+  // batches of 8 rows (4 when both the residual and the mean accumulator are loaded)
+  constexpr int IBF = ROWS_T < 8 ? ROWS_T : 8, IBM = ROWS_T < 4 ? ROWS_T : 4;
+  static_assert(ROWS_T % IBF == 0 && ROWS_T % IBM == 0, "epilogue batches");
 #pragma unroll 1
-    for (int rb = 0; rb < ROWS_T; rb += IB) {
-      f32x4 v[IB], r[IB], m[IB];
-      long long o[IB], orow[IB];
-      bool ok[IB];
+  for (int r0 = 0; r0 < BM; r0 += RPP) {
+    if (need_m) {
 #pragma unroll
-      for (int k = 0; k < IB; ++k) {
-        const int rl = trow + (rb + k) * RSTEP;
-        const int q = q0 + r0 + rl;
-        ok[k] = q < p.Lq;
-        orow[k] = (long long)q * p.out_mul + ph;
-        o[k] = ob + orow[k] * p.ldy + co;
-        v[k] = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + c4);
-        if (ok[k] && (p.epi == EPI_GAMMA_RES || p.epi == EPI_RES)) r[k] = *reinterpret_cast<const f32x4*>(p.res + o[k]);
-        if (ok[k] && (p.mean_mode == MEAN_MID || p.mean_mode == MEAN_LAST))
-          m[k] = *reinterpret_cast<const f32x4*>(p.macc + o[k]);
-      }
+      for (int rb = 0; rb < ROWS_T; rb += IBM) batch(r0, rb, rb == 0, std::integral_constant<int, IBM>{});
+    } else {
 #pragma unroll
-      for (int k = 0; k < IB; ++k) {
-        if (!ok[k]) continue;
-        f32x4 x = v[k] + bias4;
-        if (p.round_bf16) x = round_bf16x4(x);
-        switch (p.epi) {
-          case EPI_GELU:
-#pragma unroll
-            for (int e = 0; e < 4; ++e) x[e] = gelu_f(x[e]);
-            if (p.round_bf16) x = round_bf16x4(x);
-            break;
-          case EPI_GAMMA_RES: x = r[k] + gamma4 * x; break;
-          case EPI_RES: x = r[k] + x; break;
-          case EPI_LOGCLAMP:
-#pragma unroll
-            for (int e = 0; e < 4; ++e) x[e] = logf(fmaxf(x[e], 1e-5f));
-            break;
-          default: break;
-        }
-        if (p.mean_mode == MEAN_FIRST) {
-          *reinterpret_cast<f32x4*>(p.macc + o[k]) = x;
-          continue;
-        } else if (p.mean_mode == MEAN_MID) {
-          *reinterpret_cast<f32x4*>(p.macc + o[k]) = m[k] + x;
-          continue;
-        } else if (p.mean_mode == MEAN_LAST) {
-          x = (m[k] + x) / 3.0f;
-        }
-        if (p.y) *reinterpret_cast<f32x4*>(p.y + o[k]) = x;
-        if (y6) store_planes4(y6, orow[k], p.Cout, co, x[0], x[1], x[2], x[3]);
-        if (p.y2 || y6s) {
-          f32x4 sv;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) sv[e] = silu_f(x[e]);
-          if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o[k]) = sv;
-          if (y6s) store_planes4(y6s, orow[k], p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
-        }
-      }
+      for (int rb = 0; rb < ROWS_T; rb += IBF) batch(r0, rb, rb == 0, std::integral_constant<int, IBF>{});
     }
   }
 }

@@ -24,7 +24,9 @@ T = 937
 SHAPES = {"res512_k3": (512, 512, 3, 1, 32, 8 * T), "res512_k11d5": (512, 512, 11, 5, 32, 8 * T),
           "res256_k7d3": (256, 256, 7, 3, 32, 32 * T), "pw_1024": (1024, 4096, 1, 1, 1, 32 * T),
           "res64_k7d3": (64, 64, 7, 3, 32, 128 * T), "res64_k3d1": (64, 64, 3, 1, 32, 128 * T),
-          "res128_k11": (128, 128, 11, 1, 32, 64 * T), "res128_k3": (128, 128, 3, 1, 32, 64 * T)}
+          "res128_k11": (128, 128, 11, 1, 32, 64 * T), "res128_k3": (128, 128, 3, 1, 32, 64 * T),
+          "res64_k11d5": (64, 64, 11, 5, 32, 128 * T), "res32_k3d1": (32, 32, 3, 1, 32, 256 * T),
+          "res32_k11d5": (32, 32, 11, 5, 32, 256 * T)}
 
 
 def main():
@@ -56,8 +58,12 @@ def main():
         ms = e0.elapsed_time(e1) / a.reps
         mt, rt, steps = out[0], out[1], out[2]
         cyc = mt / max(steps, 1)
-        print(f"{name:14s} {ms:8.3f} ms  in-loop clock {mt / max(rt, 1) * 100.0:5.0f} MHz  "
-              f"cycles/step {cyc:6.0f}  MFMA eff {1536 / cyc:.3f}", flush=True)
+        clk = mt / max(rt, 1) * 100e6
+        # loop share: workgroup-cycles inside the main loop per CU over the kernel's wall cycles
+        # (can exceed 1 when two workgroups share a CU)
+        share = mt / 256 / max(ms * 1e-3 * a.reps * clk, 1)
+        print(f"{name:14s} {ms:8.3f} ms  in-loop clock {clk / 1e6:5.0f} MHz  "
+              f"cycles/step {cyc:6.0f}  MFMA eff {1536 / cyc:.3f}  loop share {share:.2f}", flush=True)
 
 
 if __name__ == "__main__":
