@@ -110,6 +110,28 @@ extern "C" int dcx_diag_seg(unsigned long long* out13, int reset) {
 #else
 #define DCX_SEGT(v)
 #endif
+#ifdef DCX_TILE_DIAG
+// Diagnostic build only: per-workgroup 100 MHz real-time stamps of x6dq tiles (entry, main loop
+// start, main loop end, exit) and the hardware ids of its CU (HW_ID, XCC_ID), in completion order.
+constexpr int kTileDiagMax = 16384;
+__device__ unsigned long long g_tile_diag[kTileDiagMax * 6];
+__device__ unsigned int g_tile_cnt;
+extern "C" int dcx_diag_tiles(unsigned long long* out, int max_tiles, int reset) {
+  unsigned int n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_tile_cnt), sizeof n) != hipSuccess) return -1;
+  n = n < (unsigned)max_tiles ? n : (unsigned)max_tiles;
+  n = n < (unsigned)kTileDiagMax ? n : (unsigned)kTileDiagMax;
+  if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tile_diag), sizeof(unsigned long long) * 6 * n) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned int z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_tile_cnt), &z, sizeof z) != hipSuccess) return -1;
+  }
+  return (int)n;
+}
+#define DCX_TILET(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#else
+#define DCX_TILET(v)
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // Conv epilogue through LDS: the accumulator tile is written to LDS (in row passes that fit the
@@ -1655,6 +1677,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6dm(const ConvParams p) {
 // One output tile (wg = row tile * column tiles + column tile, clip b, phase ph).
 template <int BN>
 __device__ __forceinline__ void x6dq_tile(const ConvParams& p, const int wg, const int b, const int ph) {
+  DCX_TILET(tile_t0);
   constexpr int HALO = 64;
   constexpr int BM = 65536 / BN, WN = 2;
   constexpr int WR = BM / 4, WC = BN / 2, TM = WR / 16, TN = WC / 16;
@@ -1792,6 +1815,7 @@ __device__ __forceinline__ void x6dq_tile(const ConvParams& p, const int wg, con
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   seg_barrier();
+  DCX_TILET(tile_t1);
 #ifdef DCX_CLOCK_DIAG
   const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1866,7 +1890,22 @@ __device__ __forceinline__ void x6dq_tile(const ConvParams& p, const int wg, con
     atomicAdd(&g_clock_diag[2], 2ull * nsteps);
   }
 #endif
+  DCX_TILET(tile_t2);
   epilogue_lds<BM, BN, 4, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+#ifdef DCX_TILE_DIAG
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+    const unsigned int k = atomicAdd(&g_tile_cnt, 1u);
+    if (k < (unsigned)kTileDiagMax) {
+      unsigned long long* o = g_tile_diag + 6ull * k;
+      o[0] = tile_t0; o[1] = tile_t1; o[2] = tile_t2; o[3] = t3;
+      o[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      o[5] = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+    }
+  }
+#endif
 }
 
 template <int BN>
