@@ -941,7 +941,10 @@ int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int3
   RUN(sub([&](Bump& t) { return stage_encode(h, CAct(mel), B, T, feat, t, s); }));
   RUN(sub([&](Bump& t) { return stage_vq_encode(h, CAct(feat), B, T, codes, nullptr, nullptr, nullptr, t, s); }));
   RUN(sub([&](Bump& t) { return stage_vq_decode(h, codes, B, T, z, nullptr, t, s); }));
-  RUN(sub([&](Bump& t) { return stage_generate(h, CAct(z), B, T, wav, t, s); }));
+  // a finalized handle without generator weights can never run the generator: leave it out of
+  // the workspace size (token extraction at C3's 256 clips would otherwise reserve 139 GB)
+  if (!(ws.dry && h->finalized && !h->has_gen))
+    RUN(sub([&](Bump& t) { return stage_generate(h, CAct(z), B, T, wav, t, s); }));
   if (ws.dry) ws.off = need;
   return DCX_OK;
 }

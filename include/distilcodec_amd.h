@@ -85,7 +85,8 @@ int dcx_finalize(dcx_codec* h, int32_t with_generator);
 /* Frames for a padded clip of n_samples (= raw length + 1, distil_codec.py:133-136):
  * T = floor((n_samples + 2*384 - 1024)/256) + 1. */
 int64_t dcx_num_frames(const dcx_codec* h, int64_t n_samples);
-/* Bytes of device workspace any stage call needs for batch B and T frames. */
+/* Bytes of device workspace any stage call needs for batch B and T frames.  After dcx_finalize
+ * without the generator, the generator's share (13 buffers of B*T*8192 values) is left out. */
 size_t dcx_workspace_size(const dcx_codec* h, int32_t batch, int64_t frames);
 
 /* log-mel front end.  Replaces LogMelSpectrogram.forward (mel_spec.py:109-122) incl. the

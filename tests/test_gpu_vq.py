@@ -103,3 +103,11 @@ def test_search_duplicate_codes_lowest_index(cfg, state):
         assert codes[i] == expect[int(codes0[i])]
     rows, n = eng.vq_rescore_stats()
     assert rows >= len(hit) and n >= 128 * len(hit)
+
+
+def test_workspace_without_generator(veng):
+    # a handle finalized without generator weights sizes its workspace for encode + VQ only
+    # (the generator's 13 buffers of B*T*8192 values are about 16 GB at 32 x 10 s)
+    ws = int(veng.L.dcx_workspace_size(veng.h, 32, 937))
+    gen = (5 * 4 + 8 * 6) * 32 * 937 * 8192
+    assert 0 < ws < gen // 3
