@@ -75,6 +75,7 @@ SIGNATURES = {
     "dcx_generate": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _SZ, _P]),
     "dcx_encode_decode": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _SZ, _P]),
     "dcx_transpose": (ctypes.c_int, [_P, _P, _I32, _I64, _I64, _P]),
+    "dcx_resample_poly": (ctypes.c_int, [_P, _I32, _I64, _I64, _P, _I32, _I32, _I32, _I64, _P, _I64, _I64, _P]),
     "dcx_set_gemm_mode": (ctypes.c_int, [_P, _I32]),
     "dcx_get_gemm_mode": (_I32, [_P]),
     "dcx_conv_create": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, ctypes.POINTER(_P)]),

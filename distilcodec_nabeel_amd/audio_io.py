@@ -4,8 +4,8 @@ The reference reads files with `librosa.load(path, sr=24000)` (`distilcodec/mode
 and writes them with `soundfile.write` (`distil_codec.py:640-654`); neither library exists in this
 image.  This module reads/writes RIFF/WAVE PCM (8/16/24/32-bit integer and 32-bit float) with the
 standard library, scaling integers like libsndfile (int16 / 32768) and averaging channels to mono
-like librosa.  Resampling (librosa soxr_hq) is not implemented: a file whose rate differs from the
-model's raises ValueError (SURVEY.md §8(f) rank 1 -- the file front end is the next row).
+like librosa.  A file at another rate is resampled on the GPU by `resample.py` (a polyphase FIR in
+scipy.signal.resample_poly's form, not librosa's soxr_hq).
 """
 from __future__ import annotations
 
@@ -62,13 +62,22 @@ def read_wav(path: str) -> tuple[np.ndarray, int]:
     return x.reshape(-1, ch), sr
 
 
-def load_wav(path: str, sr: int) -> tuple[np.ndarray, int]:
-    """`load_wav(full_path, sr)` (meldataset.py:18-20): mono float32 at `sr`."""
+def load_wav_mono(path: str) -> tuple[np.ndarray, int]:
+    """Mono float32 samples (channel mean, as librosa.load(mono=True)) and the file's rate."""
     x, file_sr = read_wav(path)
     x = x.mean(axis=1) if x.shape[1] > 1 else x[:, 0]
+    return np.ascontiguousarray(x, dtype=np.float32), file_sr
+
+
+def load_wav(path: str, sr: int) -> tuple[np.ndarray, int]:
+    """`load_wav(full_path, sr)` (meldataset.py:18-20): mono float32 at `sr`, resampled on the GPU
+    (distilcodec_nabeel_amd/resample.py) when the file has another rate."""
+    x, file_sr = load_wav_mono(path)
     if file_sr != sr:
-        raise ValueError(f"{file_sr} SR doesn't match target {sr} SR (resampling is not implemented)")
-    return np.ascontiguousarray(x, dtype=np.float32), sr
+        from . import resample
+
+        x = resample.resample(x, file_sr, sr).cpu().numpy()
+    return x, sr
 
 
 def write_wav(path: str, audio: np.ndarray, sr: int) -> None:

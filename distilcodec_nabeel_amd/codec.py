@@ -26,7 +26,7 @@ from functools import reduce
 import numpy as np
 import torch
 
-from . import audio_io, tokens, weights
+from . import audio_io, resample, tokens, weights
 from .config import check_supported
 from .engine import NativeCodec
 
@@ -203,6 +203,11 @@ class DistilCodec:
     def eval(self):
         return self
 
+    def _dev(self) -> torch.device:
+        if self.device is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        return self.device
+
     def _engine(self) -> NativeCodec:
         if self._eng is None:
             if self.device is None:
@@ -249,11 +254,11 @@ class DistilCodec:
     def preprocess_raw_audio_batch(self, audio_data_info_list: list):
         """distil_codec.py:99-145: items are [audio (samples,) or (channels, samples), sr]."""
         audio_list = []
+        sr_target = self.spec_config.sampling_rate
         for audio, sampling_rate in audio_data_info_list:
-            if sampling_rate != self.spec_config.sampling_rate:
-                raise ValueError(f"{sampling_rate} SR doesn't match target {self.spec_config.sampling_rate} SR "
-                                 "(resampling is not implemented on the native path)")
             a = np.asarray(audio, dtype=np.float32)
+            if sampling_rate != sr_target:  # :108-110, librosa.resample along the last axis (resample.py)
+                a = resample.resample(a, int(sampling_rate), sr_target, self._dev()).cpu().numpy()
             if a.ndim == 2:
                 a = a.mean(axis=0) if a.shape[0] > 1 else a[0]
             audio_list.append(a)
@@ -266,15 +271,15 @@ class DistilCodec:
         sr_target = self.spec_config.sampling_rate
         for p in audio_pathes:
             try:
-                audio, sampling_rate = audio_io.load_wav(p, sr=sr_target)
+                audio, sampling_rate = audio_io.load_wav_mono(p)
             except ValueError:
                 raise
             except Exception:
                 print(f"Error on audio: {p}")
                 audio = (np.random.normal(size=(sr_target,)) * 0.05).astype(np.float32)
                 sampling_rate = sr_target
-            if sampling_rate != sr_target:
-                raise ValueError("{} SR doesn't match target {} SR".format(sampling_rate, sr_target))
+            if sampling_rate != sr_target:  # librosa.load(path, sr=24000) resamples the mono signal
+                audio = resample.resample(audio, sampling_rate, sr_target, self._dev()).cpu().numpy()
             audio_list.append(np.asarray(audio, np.float32))
         return self._finish_preprocess(audio_list)
 
@@ -377,7 +382,7 @@ class DistilCodec:
 
 # -------------------------------------------------------------------- module-level helpers
 def load_and_resample_audio(file_path, target_sr, mono=True, limited=None):
-    """distil_codec.py:657-684 (WAV input only; no resampling)."""
+    """distil_codec.py:657-684 (WAV input; every channel resampled on the GPU, then the mean)."""
     y, orig_sr = audio_io.read_wav(file_path)
     y = y.T  # (channels, samples) like librosa.load(mono=False)
     audio_duration = y.shape[1] / orig_sr
@@ -385,7 +390,7 @@ def load_and_resample_audio(file_path, target_sr, mono=True, limited=None):
         start = np.random.randint(0, y.shape[1] - int(orig_sr * limited))
         y = y[:, start: start + int(orig_sr * limited)]
     if orig_sr != target_sr:
-        raise ValueError(f"{orig_sr} SR doesn't match target {target_sr} SR (resampling is not implemented)")
+        y = resample.resample(y, orig_sr, target_sr).cpu().numpy()
     if mono and y.shape[0] > 1:
         y = np.mean(y, axis=0, keepdims=True)
     return y.astype(np.float32), target_sr, audio_duration

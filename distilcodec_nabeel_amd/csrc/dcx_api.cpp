@@ -1253,6 +1253,20 @@ int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int6
   return dcx::launch_transpose(in, out, batch, rows, cols, (hipStream_t)stream) == hipSuccess ? DCX_OK : DCX_ERR_HIP;
 }
 
+int dcx_resample_poly(const float* x, int32_t batch, int64_t n_in, int64_t x_stride, const double* h, int32_t h_len,
+                      int32_t up, int32_t down, int64_t pre, float* y, int64_t n_out, int64_t y_stride, void* stream) {
+  if (!x || !h || !y || batch <= 0 || n_in <= 0 || n_out <= 0 || h_len <= 0 || up <= 0 || down <= 0 || pre < 0 ||
+      x_stride < n_in || y_stride < n_out || batch > 65535)
+    return DCX_ERR_INVALID_ARG;
+  // the largest filter index a thread can form must fit: t - up * m_lo < h_len by construction;
+  // t itself must not overflow
+  if ((pre + n_out) > (INT64_MAX / down)) return DCX_ERR_INVALID_ARG;
+  return dcx::launch_resample_poly(x, batch, n_in, x_stride, h, h_len, up, down, pre, y, n_out, y_stride,
+                                   (hipStream_t)stream) == hipSuccess
+             ? DCX_OK
+             : DCX_ERR_HIP;
+}
+
 int dcx_set_gemm_mode(dcx_codec* h, int32_t mode) {
   if (!h) return DCX_ERR_INVALID_ARG;
   if (mode != DCX_GEMM_F32 && mode != DCX_GEMM_X6 && mode != DCX_GEMM_BF16)

@@ -106,5 +106,8 @@ hipError_t launch_gather_rows(const float* table, int ntable, const int32_t* idx
 hipError_t launch_conv_post_tanh(const float* x, const float* w, float bias, float* out, int batch, int L, int C,
                                  int k, hipStream_t s);
 hipError_t launch_transpose(const float* in, float* out, int batch, long long rows, long long cols, hipStream_t s);
+hipError_t launch_resample_poly(const float* x, int batch, long long n_in, long long xs, const double* h, int hlen,
+                                int up, int down, long long pre, float* y, long long n_out, long long ys,
+                                hipStream_t s);
 
 }  // namespace dcx

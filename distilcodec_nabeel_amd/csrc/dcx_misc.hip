@@ -526,4 +526,36 @@ hipError_t launch_transpose(const float* in, float* out, int batch, long long ro
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// Sample-rate conversion by up / down (the reference resamples with librosa.resample on input
+// audio at another rate: distil_codec.py:108-110, 676; meldataset.py:18-20).  Polyphase FIR in the
+// form of scipy.signal.resample_poly (upfirdn of the zero-stuffed input, h pre-padded, output
+// window starting at `pre`):
+//   y[b][i] = sum_m h[t - up * m] * x[b][m],   t = (i + pre) * down,   0 <= t - up * m < hlen, 0 <= m < n_in
+// One thread per output sample, fp64 taps and accumulation (20-60 taps per output, the work is
+// tiny next to the HBM traffic), fp32 output.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) resample_poly_kernel(const float* __restrict__ x, long long n_in, long long xs,
+                                                            const double* __restrict__ h, int hlen, int up, int down,
+                                                            long long pre, float* __restrict__ y, long long n_out,
+                                                            long long ys) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_out) return;
+  const float* __restrict__ xb = x + (long long)blockIdx.y * xs;
+  const long long t = (i + pre) * down;
+  const long long m_hi = min(t / up, n_in - 1);
+  const long long m_lo = t - (hlen - 1) <= 0 ? 0 : (t - (hlen - 1) + up - 1) / up;
+  double acc = 0.0;
+  for (long long m = m_lo; m <= m_hi; ++m) acc = fma(h[t - up * m], (double)xb[m], acc);
+  y[(long long)blockIdx.y * ys + i] = (float)acc;
+}
+
+hipError_t launch_resample_poly(const float* x, int batch, long long n_in, long long xs, const double* h, int hlen,
+                                int up, int down, long long pre, float* y, long long n_out, long long ys,
+                                hipStream_t s) {
+  const dim3 grid((unsigned)((n_out + 255) / 256), (unsigned)batch);
+  hipLaunchKernelGGL(resample_poly_kernel, grid, dim3(256), 0, s, x, n_in, xs, h, hlen, up, down, pre, y, n_out, ys);
+  return hipGetLastError();
+}
+
 }  // namespace dcx

@@ -124,6 +124,15 @@ int dcx_generate(dcx_codec* h, const float* z, int32_t batch, int64_t frames, fl
 int dcx_encode_decode(dcx_codec* h, const float* audio, int32_t batch, int64_t n_samples,
                       int32_t* codes, float* wav, void* workspace, size_t ws_bytes, void* stream);
 
+/* Sample-rate conversion by up/down for input audio at another rate (replaces librosa.resample,
+ * distil_codec.py:108-110 and :676, and librosa.load(sr=...) in meldataset.py:18-20).  Polyphase FIR
+ * in scipy.signal.resample_poly's form: y[b][i] = sum_m h[(i + pre)*down - up*m] * x[b][m] over the
+ * taps inside h, fp64 taps and accumulation.  The caller designs h (distilcodec_nabeel_amd/resample.py:
+ * Kaiser-windowed sinc, resample_poly's defaults) and passes it in device memory.  Rows of x and y
+ * start x_stride / y_stride floats apart; batch <= 65535. */
+int dcx_resample_poly(const float* x, int32_t batch, int64_t n_in, int64_t x_stride, const double* h, int32_t h_len,
+                      int32_t up, int32_t down, int64_t pre, float* y, int64_t n_out, int64_t y_stride, void* stream);
+
 /* Batched 2-D transpose [B][R][C] -> [B][C][R] (channels-first <-> channels-last bridge). */
 int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int64_t cols, void* stream);
 
