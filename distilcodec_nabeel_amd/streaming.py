@@ -3,9 +3,8 @@
 BASELINE.json configs[4] / SURVEY.md §8(d) C5: 1 s hops (24,000 samples -> 93 frames -> 23,808
 output samples), B = 1, one hipGraph-captured step, p50/p99 latency. Each hop is encoded and
 decoded on its own, exactly as the reference does for a 1 s clip
-(`DistilCodec.encode` + `decode_from_codes`, distil_codec.py:545-594). The halo-overlapped
-streaming that would make chunked output equal full-clip output is SURVEY §8(f) rank 4 and is not
-done here.
+(`DistilCodec.encode` + `decode_from_codes`, distil_codec.py:545-594). `HaloStream` below is the
+halo-overlapped variant whose chunked output equals the full-clip output.
 
 The C-ABI stage calls allocate nothing and never synchronise (include/distilcodec_amd.h), so a
 whole `dcx_encode_decode` call is captured by `torch.cuda.graph` as it is launched: every kernel
@@ -55,3 +54,113 @@ class GraphedHop:
         self.audio[:, 1:].copy_(chunk, non_blocking=True)
         self.graph.replay()
         return self.codes, self.wav
+
+
+def receptive_field(cfg: dict) -> tuple[int, int]:
+    """(encoder, decoder) half receptive fields in frames, rounded up, for the architecture in `cfg`
+    (about ±60 and ±21).  Encoder: the stem conv plus one depthwise conv
+    per ConvNeXt block (encoders.py:21-60) and the quantizer's down block (grfvq.py:105-132).
+    Decoder: the quantizer's up block, conv_pre, each stage's ConvTranspose and ResBlocks
+    (generators.py:29-147), conv_post, each converted to frames at its stage's rate."""
+    import math
+
+    enc, q, dec = cfg["encoder"], cfg["quantizer"], cfg["decoder"]
+    dw = 3  # ConvNeXt depthwise k7
+    e = enc.get("kernel_size", 7) // 2 + dw * sum(enc["depths"]) + dw  # + the down block
+    hop = 1
+    for r in dec["upsample_rates"]:
+        hop *= r
+    d = dw + dec.get("pre_conv_kernel_size", 13) // 2  # up block + conv_pre (frame rate)
+    rate = 1
+    for r, k in zip(dec["upsample_rates"], dec["upsample_kernel_sizes"]):
+        d += math.ceil(k / r / 2) / rate  # ConvTranspose: its input samples, at `rate` per frame
+        rate *= r
+        res = max(sum(dd * (kk - 1) // 2 + (kk - 1) // 2 for dd in dils)
+                  for kk, dils in zip(dec["resblock_kernel_sizes"], dec["resblock_dilation_sizes"]))
+        d += res / rate
+    d += dec.get("post_conv_kernel_size", 13) // 2 / hop
+    return int(e), int(math.ceil(d))
+
+
+class HaloStream:
+    """Streaming encode -> decode whose output equals the full-clip result.
+
+    `push(chunk)` appends samples and returns the waveform samples that became final; `flush()`
+    ends the stream and returns the rest.  A frame's code is final once its encoder receptive field
+    (`enc_halo` frames each side, plus the 2 / 3 mel frames a segment edge reflects) has arrived;
+    a frame's audio is final once the codes `gen_halo` frames around it are.  Each step runs the
+    stage kernels on a window: mel + encoder + VQ from `enc_halo + 2` frames before the first new
+    code to the end of the received audio, and VQ decode + generator over the new frames plus
+    `gen_halo` on each side.  Inside a window the clip edges are the true clip edges (the
+    reference's leading zero sample, reflect padding at the end on `flush`), so every emitted
+    frame sees the same inputs as in a full-clip run.  Latency: about enc_halo + gen_halo + 3
+    frames of look-ahead.  Results equal the full clip up to fp32 summation order (window lengths
+    pick other conv tilings).
+    """
+
+    def __init__(self, engine: NativeCodec, enc_halo: int | None = None, gen_halo: int | None = None,
+                 record_codes: bool = False):
+        self.engine = engine
+        self.code_log = [] if record_codes else None  # every final code, in order (tests / token output)
+        e, d = receptive_field(engine.cfg)
+        self.enc_halo = e if enc_halo is None else enc_halo
+        self.gen_halo = d if gen_halo is None else gen_halo
+        self.hop = engine.hop
+        # only the still-needed tails are kept: audio from sample a_off (a multiple of 256, in the
+        # coordinates of the padded clip, whose sample 0 is the reference's leading zero), codes
+        # from frame c_off
+        self.audio = torch.zeros(1, device=engine.device)
+        self.a_off = 0
+        self.codes = torch.empty(0, dtype=torch.int32, device=engine.device)
+        self.c_off = 0
+        self.emitted = 0  # frames whose audio was returned
+        self.done = False
+
+    @property
+    def n_codes(self) -> int:
+        return self.c_off + self.codes.numel()
+
+    def _final_codes(self, final: bool) -> int:
+        n = self.a_off + self.audio.numel()
+        if final:
+            return self.engine.num_frames(n)
+        avail = (n - 640) // 256 + 1 if n >= 640 else 0  # mel frames with no reflected sample
+        return max(0, avail - self.enc_halo)
+
+    def _advance(self, final: bool) -> torch.Tensor:
+        eng = self.engine
+        c_done, c_new = self.n_codes, self._final_codes(final)
+        if c_new > c_done:
+            a = max(0, c_done - self.enc_halo - 2)
+            seg = self.audio[256 * a - self.a_off:].unsqueeze(0)
+            feat = eng.encode(eng.mel(seg))
+            codes = eng.vq_encode(feat, want_pjt_in=False, want_fup=False, want_quantized=False)[0][0]
+            new_codes = codes[c_done - a:c_new - a]
+            self.codes = torch.cat([self.codes, new_codes])
+            if self.code_log is not None:
+                self.code_log.append(new_codes)
+            keep = 256 * max(0, c_new - self.enc_halo - 2)  # the next window's first sample
+            self.audio = self.audio[keep - self.a_off:]
+            self.a_off = keep
+        T = self.n_codes
+        f_new = T if final else max(self.emitted, T - self.gen_halo)
+        if f_new <= self.emitted:
+            return torch.empty(0, device=eng.device)
+        g0, g1 = max(0, self.emitted - self.gen_halo), min(T, f_new + self.gen_halo)
+        wav = eng.generate(eng.vq_decode(self.codes[g0 - self.c_off:g1 - self.c_off].unsqueeze(0)))[0]
+        out = wav[self.hop * (self.emitted - g0):self.hop * (f_new - g0)]
+        self.emitted = f_new
+        drop = max(0, f_new - self.gen_halo) - self.c_off
+        self.codes, self.c_off = self.codes[drop:], self.c_off + drop
+        return out
+
+    def push(self, chunk) -> torch.Tensor:
+        if self.done:
+            raise RuntimeError("push after flush")
+        chunk = torch.as_tensor(chunk, dtype=torch.float32).to(self.engine.device).reshape(-1)
+        self.audio = torch.cat([self.audio, chunk])
+        return self._advance(final=False)
+
+    def flush(self) -> torch.Tensor:
+        self.done = True
+        return self._advance(final=True)

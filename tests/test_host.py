@@ -114,3 +114,10 @@ def test_synthetic_clips_deterministic():
     b = synth.clips(3, 4000, seed=3, kind="mix")
     assert all(np.array_equal(x, y) for x, y in zip(a, b))
     assert all(np.abs(x).max() < 1 for x in a)
+
+
+def test_stream_receptive_field(cfg):
+    # SURVEY.md §8(f) rank 4 quotes about +-60 encoder and +-21 decoder frames
+    from distilcodec_nabeel_amd import streaming
+
+    assert streaming.receptive_field(cfg) == (60, 22)
