@@ -96,19 +96,25 @@ __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict_
   const long long bidx = row / L;
   const int t = (int)(row - bidx * L);
   const float* xb = x + bidx * (long long)L * C;
+  // all 7 taps' loads unconditional (row clamped, out-of-range products dropped by a select):
+  // loads inside the range branches were each followed by a vmcnt(0), one round trip per tap
   f32x4 v[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (lane + 64 * i) * 4;
+    f32x4 xv[7], wv[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int tt = min(max(t + j - 3, 0), L - 1);
+      xv[j] = *reinterpret_cast<const f32x4*>(xb + (long long)tt * C + c);
+      wv[j] = *reinterpret_cast<const f32x4*>(dww + j * C + c);
+    }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 7; ++j) {
       const int tt = t + j - 3;
-      if (tt >= 0 && tt < L) {
-        const f32x4 xv = *reinterpret_cast<const f32x4*>(xb + (long long)tt * C + c);
-        const f32x4 wv = *reinterpret_cast<const f32x4*>(dww + j * C + c);
-        acc += xv * wv;
-      }
+      const f32x4 pr = xv[j] * wv[j];
+      if (tt >= 0 && tt < L) acc += pr;
     }
     v[i] = acc + *reinterpret_cast<const f32x4*>(dwb + c);
   }
