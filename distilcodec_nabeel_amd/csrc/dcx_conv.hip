@@ -3,7 +3,7 @@
 // One kernel family serves every contraction on the DistilCodec path:
 //   Conv1d k>1 / dilated (stem k7, conv_pre k13, ResBlock1 k3/7/11 x dil 1/3/5),
 //   1x1 convs and nn.Linear (taps = 1), ConvTranspose1d as `stride` polyphase convs
-//   (phase = blockIdx.z), the STFT as a 4-tap conv over 256-sample rows, the mel matmul,
+//   (one tile range per phase, flat_tile), the STFT as a 4-tap conv over 256-sample rows, the mel matmul,
 //   and the VQ distance GEMM (argmin epilogue, never materialising rows x 32768).
 //
 // GEMM view: rows = output time positions q (M), cols = output channels (N),
@@ -73,6 +73,18 @@ __device__ __forceinline__ float gelu_f(float v) { return 0.5f * v * (1.0f + erf
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// 1-D conv grids: tiles of (phase, clip, row tile, column tile), column tile fastest, XCD-remapped as
+// one range, so the blocks of an XCD share input panels and weights across clips too.  (With a
+// (tiles, batch, phases) grid, blockIdx.x & 7 is not the block's XCD unless tiles % 8 == 0.)
+__device__ __forceinline__ void flat_tile(int tpc, int batch, int& wg, int& b, int& ph) {
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_ph = tpc * batch;
+  ph = t / per_ph;
+  const int r = t - ph * per_ph;
+  b = r / tpc;
+  wg = r - b * tpc;
 }
 
 // Zero page read in place of out-of-range input rows (conv zero padding): selecting the address
@@ -438,10 +450,10 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const ConvParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int ntiles = p.Cout / BN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  int wg, b, ph;
+  flat_tile(((p.Lq + BM - 1) / BM) * ntiles, p.batch, wg, b, ph);
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
-  const int b = blockIdx.y, ph = blockIdx.z;
   const float* __restrict__ xb = p.x + (long long)b * p.x_bstride;
   const float* __restrict__ wp = p.w + (long long)ph * p.w_phase_stride + (long long)co0 * p.taps * p.Cin;
   const int inb = p.in_base[ph];
@@ -895,10 +907,10 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
   const int group = __builtin_amdgcn_readfirstlane(tid >> 8), gt = tid & 255;
   const int wm = wave / WN, wn = wave % WN;
   const int ntiles = p.Cout / BN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  int wg, b, ph;
+  flat_tile(((p.Lq + BM - 1) / BM) * ntiles, p.batch, wg, b, ph);
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
-  const int b = blockIdx.y, ph = blockIdx.z;
   const unsigned short* __restrict__ xb6 = AF32 ? nullptr : p.x6 + (long long)b * p.x_bstride * 3;
   const float* __restrict__ xbf = AF32 ? p.x + (long long)b * p.x_bstride : nullptr;
   const long long ldx6 = (long long)p.ldx * 3;
@@ -1182,10 +1194,10 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6lm(const ConvParams p) {
   const int group = __builtin_amdgcn_readfirstlane(tid >> 8), gt = tid & 255;
   const int wm = wave / WN, wn = wave % WN;
   const int ntiles = p.Cout / BN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  int wg, b, ph;
+  flat_tile(((p.Lq + BM - 1) / BM) * ntiles, p.batch, wg, b, ph);
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
-  const int b = blockIdx.y, ph = blockIdx.z;
   const unsigned short* __restrict__ xb6 = p.x6 + (long long)b * p.x_bstride * 3;
   const long long ldx6 = (long long)p.ldx * 3;
   const int nchunks = p.Cin / BK;
@@ -1408,13 +1420,16 @@ static hipError_t launch_x6pp(const ConvParams& p, int batch, int phases, hipStr
   // (BN = 256 needs 128 accumulator + 72 fragment VGPRs and spills at 2 waves per SIMD).  1-tap
   // convs take conv_gemm_x6lm (loads spread through the MFMA segments): 151 -> 161 TF/s at
   // 1024 -> 4096; with a halo it measured equal at k11 and 4-5 % slower at k3 / taps 2.
-  const dim3 grid(((p.Lq + 255) / 256) * (p.Cout / 128), batch, phases);
+  const dim3 grid((unsigned)(((p.Lq + 255) / 256) * (p.Cout / 128) * batch * phases));
+  ConvParams q = p;
+  q.batch = batch;
+  q.phases = phases;
   if constexpr (HALO == 0) {
     if (kname) *kname = "conv_gemm_x6lm<256,128>";
-    hipLaunchKernelGGL((conv_gemm_x6lm<0>), grid, dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_gemm_x6lm<0>), grid, dim3(512), 0, s, q);
   } else {
     if (kname) *kname = "conv_gemm_x6pp<256,128,halo>";
-    hipLaunchKernelGGL((conv_gemm_x6pp<HALO, 128>), grid, dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_gemm_x6pp<HALO, 128>), grid, dim3(512), 0, s, q);
   }
   return hipGetLastError();
 }
@@ -1481,10 +1496,10 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6dm(const ConvParams p) {
   const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
   const int wm = wave >> 1, wn = wave & 1;
   const int ntiles = p.Cout / BN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  int wg, b, ph;
+  flat_tile(((p.Lq + BM - 1) / BM) * ntiles, p.batch, wg, b, ph);
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
-  const int b = blockIdx.y, ph = blockIdx.z;
   const int nchunks = p.Cin / BK;
   const int taps = p.taps;
   const int nsteps = nchunks * taps;
@@ -1910,7 +1925,9 @@ __device__ __forceinline__ void x6dq_tile(const ConvParams& p, const int wg, con
 
 template <int BN>
 __global__ void __launch_bounds__(512, 2) conv_gemm_x6dq(const ConvParams p) {
-  x6dq_tile<BN>(p, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y, blockIdx.z);
+  int wg, b, ph;
+  flat_tile(((p.Lq + 65536 / BN - 1) / (65536 / BN)) * (p.Cout / BN), p.batch, wg, b, ph);
+  x6dq_tile<BN>(p, wg, b, ph);
 }
 
 // Grouped launch: up to 3 independent convs with the same tiling (the three ResBlocks' convs of one
@@ -1936,9 +1953,12 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6dq_group(const ConvGroup g
 template <int BN>
 static hipError_t launch_x6dq(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
   constexpr int BM = 65536 / BN;
-  const dim3 grid(((p.Lq + BM - 1) / BM) * (p.Cout / BN), batch, phases);
+  const dim3 grid((unsigned)(((p.Lq + BM - 1) / BM) * (p.Cout / BN) * batch * phases));
+  ConvParams q = p;
+  q.batch = batch;
+  q.phases = phases;
   if (kname) *kname = BN == 256 ? "conv_gemm_x6dq<256,256,halo>" : "conv_gemm_x6dq<512,128,halo>";
-  hipLaunchKernelGGL((conv_gemm_x6dq<BN>), grid, dim3(512), 0, s, p);
+  hipLaunchKernelGGL((conv_gemm_x6dq<BN>), grid, dim3(512), 0, s, q);
   return hipGetLastError();
 }
 
@@ -1966,10 +1986,10 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
   const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
   const int wm = wave / WN, wn = wave % WN;
   const int ntiles = p.Cout / BN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  int wg, b, ph;
+  flat_tile(((p.Lq + BM - 1) / BM) * ntiles, p.batch, wg, b, ph);
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
-  const int b = blockIdx.y, ph = blockIdx.z;
   const int nsteps = p.Cin / 32;
   const int arow = p.ldx * 6;
   const int row0 = q0 + p.in_base[ph];  // >= 0 for 1x1 convs; the descriptor covers the tile's rows
@@ -2110,10 +2130,13 @@ static bool big_tiles_pay(const ConvParams& p, int phases, int bn) {
 template <int HALO, int BN>
 static hipError_t launch_x6dm(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
   constexpr int BM = 65536 / BN;
-  const dim3 grid(((p.Lq + BM - 1) / BM) * (p.Cout / BN), batch, phases);
+  const dim3 grid((unsigned)(((p.Lq + BM - 1) / BM) * (p.Cout / BN) * batch * phases));
+  ConvParams q = p;
+  q.batch = batch;
+  q.phases = phases;
   if (kname)
     *kname = BN == 256 ? (HALO ? "conv_gemm_x6dm<256,256,halo>" : "conv_gemm_x6dm<256,256>") : "conv_gemm_x6dm<512,128,halo>";
-  hipLaunchKernelGGL((conv_gemm_x6dm<HALO, BN>), grid, dim3(512), 0, s, p);
+  hipLaunchKernelGGL((conv_gemm_x6dm<HALO, BN>), grid, dim3(512), 0, s, q);
   return hipGetLastError();
 }
 
@@ -2464,8 +2487,11 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_dm(const ConvParams p) {
 template <int BM, int BN, int WM, int WN, bool ARGMIN>
 static hipError_t launch_f32(const ConvParams& p, int batch, int phases, hipStream_t s) {
   const int mtiles = (p.Lq + BM - 1) / BM;
-  dim3 grid(mtiles * (p.Cout / BN), batch, phases);
-  hipLaunchKernelGGL((conv_gemm_f32<BM, BN, WM, WN, ARGMIN>), grid, dim3(256), 0, s, p);
+  const dim3 grid((unsigned)(mtiles * (p.Cout / BN) * batch * phases));
+  ConvParams q = p;
+  q.batch = batch;
+  q.phases = phases;
+  hipLaunchKernelGGL((conv_gemm_f32<BM, BN, WM, WN, ARGMIN>), grid, dim3(256), 0, s, q);
   return hipGetLastError();
 }
 
@@ -2526,8 +2552,11 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
 #ifndef DCX_NO_PF
         if (!b1) {  // x6: ping-pong, 512 x 64 tiles
           if (kname) *kname = "conv_gemm_x6pf<512,64,halo>";
-          hipLaunchKernelGGL((conv_gemm_x6pp<64, 64, true>), dim3(((p.Lq + 511) / 512) * (p.Cout / 64), batch, phases),
-                             dim3(512), 0, s, p);
+          ConvParams q = p;
+          q.batch = batch;
+          q.phases = phases;
+          hipLaunchKernelGGL((conv_gemm_x6pp<64, 64, true>), dim3((unsigned)(((p.Lq + 511) / 512) * (p.Cout / 64) * batch * phases)),
+                             dim3(512), 0, s, q);
           return hipGetLastError();
         }
 #endif
@@ -2548,7 +2577,11 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
     if (b1 && !h && p.taps == 1 && p.Cout % 256 == 0 && p.Cin % 32 == 0 && big_tiles_pay(p, phases, 256) &&
         in_base_nonneg(p) && 1024LL * p.ldx * 6 < (1LL << 31) && (long long)(p.Cin / 16) * p.Cout * 96 < (1LL << 31)) {
       if (kname) *kname = "conv_gemm_bf16dm<256,256>";
-      hipLaunchKernelGGL(conv_gemm_bf16dm, dim3(((p.Lq + 255) / 256) * (p.Cout / 256), batch, phases), dim3(512), 0, s, p);
+      ConvParams q = p;
+      q.batch = batch;
+      q.phases = phases;
+      hipLaunchKernelGGL(conv_gemm_bf16dm, dim3((unsigned)(((p.Lq + 255) / 256) * (p.Cout / 256) * batch * phases)), dim3(512), 0,
+                         s, q);
       return hipGetLastError();
     }
 #endif
