@@ -144,3 +144,35 @@ def test_full_clip_against_oracle(codec, state, cfg):
     assert (gc == rc).mean() >= 0.97
     if np.array_equal(gc, rc):
         assert _snr(wav, ref["wav"][:, 0].numpy()) >= 70
+
+
+@pytest.mark.parametrize("n", [384, 511, 1000, 3001])
+def test_shortest_clips_against_oracle(codec, state, cfg, n):
+    """Clips at and just above the shortest the reference accepts (384 samples + the leading zero
+    sample: the STFT's 384-sample reflect pad, mel_spec.py) through the GPU path and the oracle."""
+    from oracle import reference_cpu as R
+
+    x = (0.1 * np.random.RandomState(n).randn(n)).astype(np.float32)
+    audio, _ = R.pad_batch([x])
+    ref = R.encode_decode(audio, state, cfg)
+    codes, wav = codec._engine().encode_decode(audio.cuda())
+    rc = ref["codes"][0, :, :, 0].numpy()
+    gc = codes.cpu().numpy().astype(np.int64)
+    assert gc.shape == rc.shape and wav.shape[-1] == ref["wav"].shape[-1]
+    best, second, _ = R.top2_gap_fp64(ref["x_pjt_in"], R.codebook(state["quantizer"]))
+    dec = (((second - best) / best) > 1e-4).numpy().reshape(rc.shape)
+    assert np.array_equal(gc[dec], rc[dec])
+    if np.array_equal(gc, rc):
+        assert _snr(wav, ref["wav"][:, 0].numpy()) >= 60
+
+
+def test_too_short_clip_raises(codec):
+    """383 samples (+ the leading zero) is inside the reflect pad: the reference's F.pad raises
+    RuntimeError; the boundary returns DCX_ERR_INVALID_ARG, raised here as ValueError."""
+    from oracle import reference_cpu as R
+
+    audio, _ = R.pad_batch([np.zeros(383, np.float32)])
+    with pytest.raises(RuntimeError):
+        R.log_mel(audio)
+    with pytest.raises(ValueError, match="too short"):
+        codec._engine().encode_decode(audio.cuda())
