@@ -54,6 +54,12 @@ def test_host_queries_and_validation(cfg):
         for n in (256, 24001, 72001, 240001):
             assert L.dcx_num_frames(h, n) == (n + 768 - 1024) // 256 + 1
         assert L.dcx_num_frames(h, 240001) == 937
+        # the shortest padded clips the reflect pad accepts: frame count equals the oracle's STFT
+        import torch
+        from oracle import reference_cpu as R
+
+        for n in (385, 386, 512, 640, 641, 1001, 3002):
+            assert L.dcx_num_frames(h, n) == R.log_mel(torch.zeros(1, n)).shape[-1], n
         ws = L.dcx_workspace_size(h, 32, 937)
         # generator: 5 fp32 buffers + 8 bf16-planes buffers (6 bytes per value) of B*T*8192 values
         gen = (5 * 4 + 8 * 6) * 32 * 937 * 8192
