@@ -1,30 +1,37 @@
 #!/usr/bin/env python3
 """Throughput benchmark of the MI355X DistilCodec encode -> VQ -> decode path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--seconds S]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-Workload (BASELINE.json configs[1], "C2"): per GPU, a batch of 32 synthetic 10 s 24 kHz clips
-(speech-like / music-like mix), fp32, the full path mel -> ConvNeXt encoder -> GRFVQ search ->
-decode(codes) -> HiFiGAN generator, i.e. `DistilCodec.encode` followed by `decode_from_codes`.
-A step = one pass of the path over the rank's batch, inputs already resident in HBM.  Clips are
-independent, so ranks shard clips with no collective on the data path (weak scaling); the only
-collectives are the timing barrier and the max-over-ranks reduction.
+Workloads (BASELINE.json configs):
+  c2 (default; configs[1]): 32 synthetic 10 s 24 kHz clips PER GPU (speech-like / music-like),
+     fp32, the full path mel -> ConvNeXt encoder -> GRFVQ search -> decode(codes) -> HiFiGAN
+     generator, i.e. `DistilCodec.encode` followed by `decode_from_codes`.
+  c4 (configs[3]): 128 ragged universal-audio clips (9-10 s, speech+music) per GPU, global batch
+     128 N (1024 on 8 GPUs), every shard padded to the GLOBAL maximum.
+Both run through the shipped multi-GPU path (`sharding.ShardedEncodeDecode`): rank r holds its
+contiguous shard of the global clip list, resident in HBM; a step = `dcx_encode_decode` over the
+shard plus the all_gather of every rank's codes (RCCL over xGMI).  Clips are independent, so there
+is no collective on the data path (weak scaling); the gather is the only exchange.  With N > 1 and
+the default c2 workload, a C4 pass is measured too and reported under "c4".
 
-Rank 0 prints one JSON line.  `roofline` reports the dominant kernel (largest summed device
-time, HIP events around each launch on its stream during the timed steps) as algorithmic
-FLOP/s against the fp32 MFMA peak; `cpu_baseline` times the CPU oracle (the reference's
-algorithm on PyTorch-CPU, oracle/reference_cpu.py) on a bounded sample on this host.
+Rank 0 prints one JSON line.  `value` counts real (unpadded) clip samples of all ranks per second.
+`roofline` reports the dominant kernel (largest summed device time, HIP events around each launch
+on its stream during the timed steps) as algorithmic FLOP/s against its MFMA ceiling;
+`cpu_baseline` times the CPU oracle (the reference's algorithm on PyTorch-CPU,
+oracle/reference_cpu.py) on a bounded sample on this host, all cores and 1 thread, median of 3.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
+import statistics
 import sys
 import time
 
-import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -32,7 +39,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 from distilcodec_nabeel_amd import config as dconfig  # noqa: E402
-from distilcodec_nabeel_amd import synth, weights  # noqa: E402
+from distilcodec_nabeel_amd import sharding, synth, weights  # noqa: E402
 from distilcodec_nabeel_amd.engine import NativeCodec  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (= fp32 vector peak)
@@ -41,6 +48,13 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
 HBM_PEAK_GBS = 8000.0
 SR = 24000
+MFLOP_PER_FRAME = 2045.08  # encode -> decode algorithmic work per 256-sample frame
+
+WORKLOADS = {
+    # clips per GPU, longest clip, shortest clip
+    "c2": (32, 240000, 240000),
+    "c4": (128, 240000, 216000),
+}
 
 
 def traffic_for(kernel: str):
@@ -55,21 +69,111 @@ def traffic_for(kernel: str):
         return None
 
 
-def cpu_baseline(cfg, state, seconds: float, batch: int):
-    """Oracle (PyTorch-CPU restatement of the reference) on a bounded sample of the workload."""
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def _host_threads() -> int:
+    """The CPU share this process may use: the affinity mask, capped by OMP_NUM_THREADS when set
+    (16 on the GPU box, whose os.cpu_count() shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
+def cpu_baseline(cfg, state):
+    """Oracle (PyTorch-CPU restatement of the reference) on bounded samples of the
+    C2 workload: 1 warm-up then the median of 3 runs, with all host threads and with 1 thread."""
     from oracle import reference_cpu as R
 
-    threads = min(16, os.cpu_count() or 1)
+    def timed(batch, n, threads, seed):
+        torch.set_num_threads(threads)
+        R.encode_decode(R.pad_batch(synth.clips(1, SR // 4, seed=999))[0], state, cfg)  # warm-up
+        audio, _ = R.pad_batch(synth.clips(batch, n, seed=seed, kind="mix"))
+        runs = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            R.encode_decode(audio, state, cfg)
+            runs.append(time.perf_counter() - t0)
+        return batch * n / statistics.median(runs), runs
+
+    threads = _host_threads()
+    v_all, runs_all = timed(2, 5 * SR, threads, 0)
+    v_one, runs_one = timed(1, SR, 1, 0)
     torch.set_num_threads(threads)
-    warm, _ = R.pad_batch(synth.clips(1, SR // 2, seed=999))
-    R.encode_decode(warm, state, cfg)
-    audio, _ = R.pad_batch(synth.clips(batch, int(seconds * SR), seed=0, kind="mix"))
+    return {"value": round(v_all, 1), "unit": "samples/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "host_cpu_count": os.cpu_count(),
+            "value_1thread": round(v_one, 1),
+            "sample": (f"full encode->VQ->decode, fp32, oracle/reference_cpu.py, 1 warm-up + median of 3: "
+                       f"{threads} threads on 2 x 5 s clips (runs {', '.join(f'{r:.2f}' for r in runs_all)} s); "
+                       f"1 thread on 1 x 1 s clip (runs {', '.join(f'{r:.2f}' for r in runs_one)} s)")}
+
+
+def make_runner(eng, workload: str, rank: int, world: int, seed: int = 0):
+    per_gpu, longest, shortest = WORKLOADS[workload]
+    n_total = per_gpu * world
+    lengths = synth.ragged_lengths(n_total, seed + 7, longest, shortest)
+    s, e = sharding.shard_bounds(n_total, rank, world)
+    clips = synth.batch_clips(lengths, s, e, seed=seed)
+    runner = sharding.ShardedEncodeDecode(eng, clips, max(lengths), n_total, rank, world)
+    return runner, sum(lengths), n_total
+
+
+def run_timed(runner, steps: int, warmup: int, world: int, dev, profile_eng=None):
+    """W untimed steps, then K steps between barrier + synchronize; max over ranks."""
+    for _ in range(warmup):
+        runner.step()
+    torch.cuda.synchronize(dev)
+    codes = runner.codes
+    if codes.numel():
+        assert int(codes.min()) >= 0 and int(codes.max()) < 32768
+        assert bool(torch.isfinite(runner.wav).all())
+    if profile_eng is not None:
+        profile_eng.profile(True)
+        profile_eng.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    R.encode_decode(audio, state, cfg)
+    for _ in range(steps):
+        all_codes, _ = runner.step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
     dt = time.perf_counter() - t0
-    return {"value": round(batch * seconds * SR / dt, 1), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{batch} x {seconds:g} s clips, full encode->VQ->decode, fp32, oracle/reference_cpu.py, "
-                      f"{dt:.1f} s wall"}
+    prof = {}
+    if profile_eng is not None:
+        prof = profile_eng.profile_read()
+        profile_eng.profile(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        assert all_codes.shape[0] == runner.n_total
+    return dt, prof
+
+
+def roofline(prof: dict, steps: int):
+    if not prof:
+        return None
+    name, rec = max(prof.items(), key=lambda kv: kv[1]["ms"])
+    avg_ms = rec["ms"] / rec["launches"]
+    achieved = rec["flops"] / (rec["ms"] * 1e-3) / 1e12
+    peak = X6_PEAK_TFLOPS if "x6" in name else FP32_MFMA_PEAK_TFLOPS
+    return {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": round(peak, 1),
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic_for(name),
+            "peak_basis": ("bf16 dense MFMA 2500 TF / 6 bf16 products per fp32 product" if "x6" in name
+                           else "fp32 MFMA v_mfma_f32_32x32x2_f32"),
+            "launches_per_step": rec["launches"] // steps, "avg_launch_ms": round(avg_ms, 4),
+            "flops_per_launch": rec["flops"] / rec["launches"],
+            "share_of_device_time": round(rec["ms"] / sum(r["ms"] for r in prof.values()), 4)}
 
 
 def main():
@@ -77,11 +181,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
-    ap.add_argument("--seconds", type=float, default=10.0, help="clip length")
+    ap.add_argument("--config", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--no-c4", action="store_true", help="skip the extra C4 pass at N > 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--no-f32", action="store_true", help="skip the IEEE fp32-MFMA comparison pass at N = 1")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch HIP-event roofline timing")
     ap.add_argument("--gemm", choices=["x6", "f32"], default="x6",
                     help="x6: fp32 operands as 3 bf16 planes, 6 exact products, f32 accumulate; f32: fp32 MFMA")
@@ -99,69 +202,46 @@ def main():
     state = weights.synthetic_state_dict(cfg, seed=1234)
     eng = NativeCodec(cfg, state, dev, gemm=args.gemm)
 
-    n = int(args.seconds * SR)
-    clips = synth.clips(args.batch, n, seed=1000 * rank, kind="mix")
-    audio = torch.zeros(args.batch, n + 1)  # reference layout: 1 leading zero (distil_codec.py:133-136)
-    for i, c in enumerate(clips):
-        audio[i, 1:] = torch.from_numpy(c)
-    audio = audio.to(dev)
-    T = eng.num_frames(n + 1)
-    codes = torch.empty(args.batch, T, dtype=torch.int32, device=dev)
-    wav = torch.empty(args.batch, 256 * T, device=dev)
-
-    for _ in range(args.warmup):
-        eng.encode_decode(audio, codes, wav)
-    torch.cuda.synchronize(dev)
-    assert int(codes.min()) >= 0 and int(codes.max()) < cfg["quantizer"]["codebook_size"]
-    assert bool(torch.isfinite(wav).all())
-
-    if not args.no_profile:
-        eng.profile(True)
-        eng.profile_reset()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.encode_decode(audio, codes, wav)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    prof = {}
-    if not args.no_profile:
-        prof = eng.profile_read()
-        eng.profile(False)
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
+    runner, samples, n_total = make_runner(eng, args.config, rank, world)
+    dt, prof = run_timed(runner, args.steps, args.warmup, world, dev, None if args.no_profile else eng)
     ms_step = dt / args.steps * 1e3
-    samples = args.batch * n * world
     value = samples / (dt / args.steps)
+    padded = n_total * (runner.audio.shape[1] - 1)
+    roof = roofline(prof, args.steps)
+    if roof and rank == 0 and os.environ.get("DCX_BENCH_KERNELS"):
+        with open(os.environ["DCX_BENCH_KERNELS"], "w") as f:
+            json.dump({"steps": args.steps, "kernels": prof}, f, indent=1)
 
-    roof = None
-    if prof:
-        name, rec = max(prof.items(), key=lambda kv: kv[1]["ms"])
-        avg_ms = rec["ms"] / rec["launches"]
-        achieved = rec["flops"] / (rec["ms"] * 1e-3) / 1e12
-        peak = X6_PEAK_TFLOPS if "x6" in name else FP32_MFMA_PEAK_TFLOPS
-        roof = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": round(peak, 1),
-                "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic_for(name),
-                "peak_basis": ("bf16 dense MFMA 2500 TF / 6 bf16 products per fp32 product" if "x6" in name
-                               else "fp32 MFMA v_mfma_f32_32x32x2_f32"),
-                "launches_per_step": rec["launches"] // args.steps, "avg_launch_ms": round(avg_ms, 4),
-                "share_of_device_time": round(rec["ms"] / sum(r["ms"] for r in prof.values()), 4)}
-        if rank == 0 and os.environ.get("DCX_BENCH_KERNELS"):
-            with open(os.environ["DCX_BENCH_KERNELS"], "w") as f:
-                json.dump({"steps": args.steps, "kernels": prof}, f, indent=1)
+    c4 = None
+    if world > 1 and args.config == "c2" and not args.no_c4:
+        r4, s4, n4 = make_runner(eng, "c4", rank, world)
+        k4 = min(args.steps, 3)
+        dt4, _ = run_timed(r4, k4, 1, world, dev)
+        c4 = {"workload": f"C4: {n4} ragged clips (9-10 s, speech+music), {n4 // world} per GPU, padded to the global max",
+              "value": round(s4 / (dt4 / k4), 1), "unit": "samples/s", "ms_per_step": round(dt4 / k4 * 1e3, 3),
+              "steps": k4, "warmup": 1, "global_batch": n4}
+        del r4
+
+    f32 = None
+    if world == 1 and args.gemm == "x6" and not args.no_f32:
+        eng.set_gemm("f32")
+        kf = min(args.steps, 2)
+        dtf, _ = run_timed(runner, kf, 1, world, dev)
+        eng.set_gemm("x6")
+        f32 = {"value": round(samples / (dtf / kf), 1), "unit": "samples/s", "ms_per_step": round(dtf / kf * 1e3, 3),
+               "steps": kf, "arith": "IEEE fp32 MFMA (v_mfma_f32_32x32x2_f32), same workload",
+               "tflops": round(samples / 256 * MFLOP_PER_FRAME * 1e6 / (dtf / kf) / 1e12, 1)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, state, args.cpu_seconds, args.cpu_batch)
+        cpu = cpu_baseline(cfg, state)
 
     if rank == 0:
+        per_gpu, longest, shortest = WORKLOADS[args.config]
+        workload = (f"C2: {per_gpu} x 10 s clips per GPU, full mel->encoder->VQ->decode->generator, fp32"
+                    if args.config == "c2" else
+                    f"C4: {n_total} ragged clips (9-10 s, speech+music), {per_gpu} per GPU, padded to the global max, "
+                    f"full path, fp32")
         out = {
             "metric": "24 kHz samples/s encode+decode at 1/8 GPU; code-index bit-exact vs CPU",
             "value": round(value, 1),
@@ -178,10 +258,13 @@ def main():
                       "accumulation (v_mfma_f32_16x16x32_bf16 / 32x32x16_bf16)" if args.gemm == "x6" else
                       "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
             "data": "synthetic (speech/music-like 24 kHz clips; seeded synthetic weights, no checkpoint offline)",
-            "config": {"workload": f"C2: {args.batch} x {args.seconds:g} s clips per GPU, full mel->encoder->VQ->"
-                                   f"decode->generator, fp32", "global_batch": args.batch * world,
-                       "clip_samples": n, "frames_per_clip": T, "parallelism": f"clip-sharded x{world}"},
+            "config": {"workload": workload, "global_batch": n_total, "clip_samples_max": longest,
+                       "frames_per_clip": runner.frames, "parallelism": f"clip-sharded x{world}, codes all_gather",
+                       "padded_samples_per_s": round(padded / (dt / args.steps), 1)},
+            "tflops_algorithmic": round(padded / 256 * MFLOP_PER_FRAME * 1e6 / (dt / args.steps) / 1e12, 1),
             "roofline": roof,
+            "f32_ieee": f32,
+            "c4": c4,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

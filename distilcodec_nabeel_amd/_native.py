@@ -8,11 +8,16 @@ one runtime, one device context and torch's streams.
 from __future__ import annotations
 
 import ctypes
+import glob
+import hashlib
 import os
 
 import torch  # noqa: F401  (see module docstring)
 
-LIB_PATH = os.environ.get("DCX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdcx.so")
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DCX_LIB") or os.path.join(_PKG, "libdcx.so")
+CSRC = os.path.join(_PKG, "csrc")
+HEADER = os.path.join(os.path.dirname(_PKG), "include", "distilcodec_amd.h")
 
 DCX_OK = 0
 DCX_ERR_INVALID_ARG = -1
@@ -64,6 +69,7 @@ SIGNATURES = {
     "dcx_last_error": (ctypes.c_char_p, [_P]),
     "dcx_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "dcx_abi_version": (ctypes.c_int, []),
+    "dcx_build_id": (ctypes.c_char_p, []),
     "dcx_set_tensor": (ctypes.c_int, [_P, ctypes.c_char_p, _P, _I32, ctypes.POINTER(_I64)]),
     "dcx_finalize": (ctypes.c_int, [_P, _I32]),
     "dcx_num_frames": (_I64, [_P, _I64]),
@@ -93,6 +99,20 @@ SIGNATURES = {
 _lib = None
 
 
+def source_build_id() -> str | None:
+    """The hash csrc/Makefile embeds in libdcx.so: SHA-256 over the library's sources in sorted
+    order (csrc/*.cpp, *.hip, *.h), then include/distilcodec_amd.h; first 16 hex digits.  None when
+    the sources are not next to the library."""
+    names = sorted(os.path.basename(p) for ext in ("cpp", "hip", "h") for p in glob.glob(os.path.join(CSRC, f"*.{ext}")))
+    if not names or not os.path.isfile(HEADER):
+        return None
+    h = hashlib.sha256()
+    for path in [os.path.join(CSRC, n) for n in names] + [HEADER]:
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def lib() -> ctypes.CDLL:
     """Load libdcx.so once; raise NativeUnavailable (never fall back) when it cannot be used."""
     global _lib
@@ -110,6 +130,13 @@ def lib() -> ctypes.CDLL:
         f.argtypes = args
     if L.dcx_abi_version() != 1:
         raise NativeUnavailable("libdcx.so ABI version mismatch")
+    # A library selected explicitly with DCX_LIB (A/B tooling, diagnostic builds) is taken as is;
+    # the in-tree library must have been built from the sources next to it.
+    if not os.environ.get("DCX_LIB"):
+        want, have = source_build_id(), L.dcx_build_id().decode()
+        if want is not None and have != want:
+            raise NativeUnavailable(f"{LIB_PATH} is stale: built from sources {have}, the sources here hash to {want}; "
+                                    f"rebuild with `make -C {CSRC}`")
     _lib = L
     return L
 

@@ -62,6 +62,30 @@ def read_wav(path: str) -> tuple[np.ndarray, int]:
     return x.reshape(-1, ch), sr
 
 
+def _is_mp3(head: bytes) -> bool:
+    """ID3v2 tag or an MPEG audio frame sync (11 set bits) at the start of the file."""
+    return head[:3] == b"ID3" or (len(head) >= 2 and head[0] == 0xFF and (head[1] & 0xE0) == 0xE0)
+
+
+def read_audio(path: str) -> tuple[np.ndarray, int]:
+    """(float32 (frames, channels), sample_rate) of a WAV or MP3 file, chosen by its leading bytes
+    (librosa.load reads both; meldataset.py:18-20)."""
+    with open(path, "rb") as f:
+        head = f.read(4)
+    if head[:4] != b"RIFF" and _is_mp3(head):
+        from . import mp3
+
+        return mp3.read_mp3(path)
+    return read_wav(path)
+
+
+def load_audio_mono(path: str) -> tuple[np.ndarray, int]:
+    """Mono float32 samples (channel mean, as librosa.load(mono=True)) and the file's rate."""
+    x, file_sr = read_audio(path)
+    x = x.mean(axis=1) if x.shape[1] > 1 else x[:, 0]
+    return np.ascontiguousarray(x, dtype=np.float32), file_sr
+
+
 def load_wav_mono(path: str) -> tuple[np.ndarray, int]:
     """Mono float32 samples (channel mean, as librosa.load(mono=True)) and the file's rate."""
     x, file_sr = read_wav(path)
@@ -72,7 +96,7 @@ def load_wav_mono(path: str) -> tuple[np.ndarray, int]:
 def load_wav(path: str, sr: int) -> tuple[np.ndarray, int]:
     """`load_wav(full_path, sr)` (meldataset.py:18-20): mono float32 at `sr`, resampled on the GPU
     (distilcodec_nabeel_amd/resample.py) when the file has another rate."""
-    x, file_sr = load_wav_mono(path)
+    x, file_sr = load_audio_mono(path)
     if file_sr != sr:
         from . import resample
 

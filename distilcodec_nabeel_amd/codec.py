@@ -145,9 +145,10 @@ class DistilCodec:
         self.tokens_id_offset = configs.get("token_id_offset", 0)
         self.gr_audio_code2token = tokens.construct_audio_code(self.ngroups, self.nresiduals,
                                                                self.quantizer_config.codebook_size, self.tokens_id_offset)
-        # The reference builds randomly initialised modules here; the native path materialises
-        # deterministic synthetic weights of the same architecture (weights.py) instead.
-        self._state = weights.synthetic_state_dict(configs, seed=seed, with_generator=not only_quantizer)
+        # The reference builds randomly initialised modules here; the native path uses
+        # deterministic synthetic weights of the same architecture (weights.py) instead, built per
+        # part on first use so that a checkpoint load never synthesises what it replaces.
+        self._state = weights.LazyState(configs, seed=seed, parts=weights.PARTS if not only_quantizer else ("encoder", "quantizer"))
         self._eng = None
         self.spec_transform = SpecTransform(self)
         self.encoder = None if only_quantizer else Encoder(self)
@@ -171,6 +172,7 @@ class DistilCodec:
             codec._state["generator"] = weights.to_numpy_state(state["generator"])
         codec._state["encoder"] = weights.to_numpy_state(state["encoder"])
         codec._state["quantizer"] = weights.to_numpy_state(state["quantizer"])
+        del state
         codec.move_to_cuda()
         return codec
 
@@ -264,24 +266,32 @@ class DistilCodec:
             audio_list.append(a)
         return self._finish_preprocess(audio_list)
 
-    def preprocess_audio_batch(self, audio_pathes: list):
-        """distil_codec.py:147-198, including its fallback of 1 s of N(0,1)*0.05 noise when a file
-        cannot be read (:155-160) and the ValueError on a sample-rate mismatch (:161-163)."""
+    def _read_audio_files(self, audio_pathes: list) -> list:
+        """The file-reading half of distil_codec.py:147-198: mono float32 per path at the model rate.
+        Like the reference (:155-160), ANY failure to read a file (missing, not audio, corrupt)
+        substitutes 1 s of N(0,1)*0.05 noise.  Resampling of another rate (librosa.load(sr=24000))
+        runs on the GPU outside that fallback, so a missing GPU still fails loudly.  The
+        reference's sample-rate ValueError (:161-163) cannot trigger after resampling; it is kept."""
         audio_list = []
         sr_target = self.spec_config.sampling_rate
         for p in audio_pathes:
             try:
-                audio, sampling_rate = audio_io.load_wav_mono(p)
-            except ValueError:
-                raise
+                audio, sampling_rate = audio_io.load_audio_mono(p)
             except Exception:
                 print(f"Error on audio: {p}")
                 audio = (np.random.normal(size=(sr_target,)) * 0.05).astype(np.float32)
                 sampling_rate = sr_target
-            if sampling_rate != sr_target:  # librosa.load(path, sr=24000) resamples the mono signal
+            if sampling_rate != sr_target:
                 audio = resample.resample(audio, sampling_rate, sr_target, self._dev()).cpu().numpy()
+                sampling_rate = sr_target
+            if sampling_rate != sr_target:
+                raise ValueError("{} SR doesn't match target {} SR".format(sampling_rate, sr_target))
             audio_list.append(np.asarray(audio, np.float32))
-        return self._finish_preprocess(audio_list)
+        return audio_list
+
+    def preprocess_audio_batch(self, audio_pathes: list):
+        """distil_codec.py:147-198 (file paths -> padded batch, mel)."""
+        return self._finish_preprocess(self._read_audio_files(audio_pathes))
 
     # ---------------------------------------------------------------- tokens
     def construct_audio_code(self, tokens_id_offset: int = 0):
@@ -381,16 +391,17 @@ class DistilCodec:
 
 
 # -------------------------------------------------------------------- module-level helpers
-def load_and_resample_audio(file_path, target_sr, mono=True, limited=None):
-    """distil_codec.py:657-684 (WAV input; every channel resampled on the GPU, then the mean)."""
-    y, orig_sr = audio_io.read_wav(file_path)
+def load_and_resample_audio(file_path, target_sr, mono=True, limited=None, device=None):
+    """distil_codec.py:657-684 (WAV or MP3 input; every channel resampled on the GPU `device`, then
+    the mean)."""
+    y, orig_sr = audio_io.read_audio(file_path)
     y = y.T  # (channels, samples) like librosa.load(mono=False)
     audio_duration = y.shape[1] / orig_sr
     if limited is not None and audio_duration > limited and y.shape[1] - int(orig_sr * limited) > 1000:
         start = np.random.randint(0, y.shape[1] - int(orig_sr * limited))
         y = y[:, start: start + int(orig_sr * limited)]
     if orig_sr != target_sr:
-        y = resample.resample(y, orig_sr, target_sr).cpu().numpy()
+        y = resample.resample(y, orig_sr, target_sr, device if device is not None else "cuda").cpu().numpy()
     if mono and y.shape[0] > 1:
         y = np.mean(y, axis=0, keepdims=True)
     return y.astype(np.float32), target_sr, audio_duration
@@ -409,5 +420,5 @@ def decode_audio(codec: DistilCodec, audio_tsr, target_sr=24000, plus_offset: bo
 
 def demo_for_generate_audio_codes(codec: DistilCodec, audio_path, target_sr=24000, plus_llm_offset=True):
     """distil_codec.py:711-727."""
-    audio_tsr, _, _ = load_and_resample_audio(file_path=audio_path, target_sr=target_sr)
+    audio_tsr, _, _ = load_and_resample_audio(file_path=audio_path, target_sr=target_sr, device=codec._dev())
     return decode_audio(codec, audio_tsr=audio_tsr, plus_offset=plus_llm_offset)

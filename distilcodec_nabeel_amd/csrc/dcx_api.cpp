@@ -968,6 +968,11 @@ extern "C" {
 
 int dcx_abi_version(void) { return DCX_ABI_VERSION; }
 
+#ifndef DCX_BUILD_ID
+#define DCX_BUILD_ID "unversioned"
+#endif
+const char* dcx_build_id(void) { return DCX_BUILD_ID; }
+
 const char* dcx_status_string(int st) {
   switch (st) {
     case DCX_OK: return "ok";

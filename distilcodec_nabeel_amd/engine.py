@@ -15,6 +15,10 @@ from . import _native
 from .config import check_supported
 
 
+# codebook EMA statistics a trained checkpoint carries (vector_quantize_pytorch.py:508-531); eval
+# never reads them, and embed_avg alone is as large as the codebook (470 MB), so they are not copied
+_TRAINING_ONLY = ("_codebook.embed_avg", "_codebook.cluster_size")
+
 GEMM_MODES = {"f32": _native.DCX_GEMM_F32, "x6": _native.DCX_GEMM_X6, "bf16": _native.DCX_GEMM_BF16}
 
 
@@ -51,6 +55,8 @@ class NativeCodec:
             self._check(self.L.dcx_set_gemm_mode(self.h, GEMM_MODES[self.gemm]))
             for part in ("encoder", "quantizer") + (("generator",) if with_generator else ()):
                 for k, v in state[part].items():
+                    if k.endswith(_TRAINING_ONLY):
+                        continue
                     a = np.ascontiguousarray(np.asarray(v, dtype=np.float32))
                     shape = (ctypes.c_int64 * max(a.ndim, 1))(*a.shape)
                     self._check(self.L.dcx_set_tensor(self.h, f"{part}.{k}".encode(), a.ctypes.data_as(ctypes.c_void_p),
@@ -84,8 +90,18 @@ class NativeCodec:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def workspace(self, batch: int, frames: int) -> torch.Tensor:
-        need = int(self.L.dcx_workspace_size(self.h, batch, frames))
+    def workspace_size(self, batch: int, frames: int) -> int:
+        return int(self.L.dcx_workspace_size(self.h, batch, frames))
+
+    def workspace(self, batch: int, frames: int, ws: torch.Tensor | None = None) -> torch.Tensor:
+        """The workspace of one stage call.  A caller-owned `ws` (e.g. the one a captured hipGraph
+        was recorded with) is checked and used as is; otherwise the engine's shared buffer, which
+        grows (is reallocated) when a call needs more."""
+        need = self.workspace_size(batch, frames)
+        if ws is not None:
+            if ws.device != self.device or ws.dtype != torch.uint8 or not ws.is_contiguous() or ws.numel() < need:
+                raise ValueError(f"workspace must be a contiguous uint8 tensor on {self.device} of >= {need} bytes")
+            return ws
         if self._ws is None or self._ws.numel() < need:
             self._ws = None
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
@@ -163,7 +179,8 @@ class NativeCodec:
             self._check(self.L.dcx_generate(self.h, self._ptr(z), B, T, self._ptr(wav), self._ptr(ws), ws.numel(), self._stream()))
         return wav
 
-    def encode_decode(self, audio: torch.Tensor, codes: torch.Tensor | None = None, wav: torch.Tensor | None = None):
+    def encode_decode(self, audio: torch.Tensor, codes: torch.Tensor | None = None, wav: torch.Tensor | None = None,
+                      ws: torch.Tensor | None = None):
         audio = self._dev(audio, torch.float32)
         B, N = audio.shape
         T = self.num_frames(N)
@@ -171,7 +188,7 @@ class NativeCodec:
             codes = torch.empty(B, T, dtype=torch.int32, device=self.device)
         if wav is None:
             wav = torch.empty(B, self.hop * T, device=self.device)
-        ws = self.workspace(B, T)
+        ws = self.workspace(B, T, ws)
         with torch.cuda.device(self.device):
             self._check(self.L.dcx_encode_decode(self.h, self._ptr(audio), B, N, self._ptr(codes), self._ptr(wav), self._ptr(ws),
                                                  ws.numel(), self._stream()))

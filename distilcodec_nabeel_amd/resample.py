@@ -55,7 +55,7 @@ _filters: dict = {}
 
 
 def _device_filter(up: int, down: int, device: torch.device) -> tuple[torch.Tensor, int]:
-    key = (up, down, str(device))
+    key = (up, down, device.index)
     if key not in _filters:
         h, pre = design(up, down)
         _filters[key] = (torch.from_numpy(h).to(device), pre)
@@ -68,6 +68,8 @@ def resample(x, sr_in: int, sr_out: int, device="cuda") -> torch.Tensor:
     dev = torch.device(device)
     if dev.type != "cuda" or not torch.cuda.is_available():
         raise _native.NativeUnavailable("resampling runs on the GPU (dcx_resample_poly); no GPU device")
+    if dev.index is None:  # normalise "cuda" to the indexed current device (filter cache, launch guard)
+        dev = torch.device("cuda", torch.cuda.current_device())
     t = torch.as_tensor(x, dtype=torch.float32).to(dev).contiguous()
     if sr_in == sr_out:
         return t.clone()
@@ -81,11 +83,12 @@ def resample(x, sr_in: int, sr_out: int, device="cuda") -> torch.Tensor:
     h, pre = _device_filter(up, down, dev)
     out = torch.empty(rows.shape[0], no, device=dev)
     L = _native.lib()
-    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    for r0 in range(0, rows.shape[0], 65535):
-        r1 = min(rows.shape[0], r0 + 65535)
-        rc = L.dcx_resample_poly(ctypes.c_void_p(rows[r0].data_ptr()), r1 - r0, n, n, ctypes.c_void_p(h.data_ptr()),
-                                 h.numel(), up, down, pre, ctypes.c_void_p(out[r0].data_ptr()), no, no, stream)
-        if rc != _native.DCX_OK:
-            raise _native.NativeError(rc, "dcx_resample_poly failed")
+    with torch.cuda.device(dev):  # the kernel launches on the current device: make it `dev`
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        for r0 in range(0, rows.shape[0], 65535):
+            r1 = min(rows.shape[0], r0 + 65535)
+            rc = L.dcx_resample_poly(ctypes.c_void_p(rows[r0].data_ptr()), r1 - r0, n, n, ctypes.c_void_p(h.data_ptr()),
+                                     h.numel(), up, down, pre, ctypes.c_void_p(out[r0].data_ptr()), no, no, stream)
+            if rc != _native.DCX_OK:
+                raise _native.NativeError(rc, "dcx_resample_poly failed")
     return out.reshape(*shape[:-1], no)

@@ -36,17 +36,20 @@ class GraphedHop:
         self.audio = torch.zeros(batch, hop_samples + 1, device=self.device)  # [:, 0] stays 0
         self.codes = torch.empty(batch, self.frames, dtype=torch.int32, device=self.device)
         self.wav = torch.empty(batch, engine.hop * self.frames, device=self.device)
-        engine.workspace(batch, self.frames)  # allocate before capture
+        # The graph records raw pointers, so it owns its workspace: the engine's shared buffer is
+        # reallocated whenever a later call on the same engine needs more (a longer clip, a
+        # HaloStream window), which would leave replays writing into freed memory.
+        self.ws = torch.empty(engine.workspace_size(batch, self.frames), dtype=torch.uint8, device=self.device)
         with torch.cuda.device(self.device):
             # one eager run (module loading, first-launch work) on a side stream, then capture
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):
-                engine.encode_decode(self.audio, self.codes, self.wav)
+                engine.encode_decode(self.audio, self.codes, self.wav, ws=self.ws)
             torch.cuda.current_stream(self.device).wait_stream(s)
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
-                engine.encode_decode(self.audio, self.codes, self.wav)
+                engine.encode_decode(self.audio, self.codes, self.wav, ws=self.ws)
 
     def __call__(self, chunk: torch.Tensor):
         if tuple(chunk.shape) != (self.batch, self.hop_samples):

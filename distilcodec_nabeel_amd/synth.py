@@ -58,3 +58,20 @@ def clips(batch: int, n: int, seed: int = 0, kind: str = "speech") -> list[np.nd
     if kind == "mix":
         return [(speech_like if i % 2 == 0 else music_like)(n, seed + i) for i in range(batch)]
     return [fn[kind](n, seed + i) for i in range(batch)]
+
+
+def ragged_lengths(n_clips: int, seed: int, max_len: int, min_len: int) -> list[int]:
+    """Deterministic clip lengths in [min_len, max_len] for a ragged batch; clip 0 has max_len, so
+    the batch maximum is known without drawing every length (C4's global padding)."""
+    r = np.random.Generator(np.random.PCG64(seed))
+    lens = r.integers(min_len, max_len + 1, size=n_clips).tolist()
+    if n_clips:
+        lens[0] = max_len
+    return [int(x) for x in lens]
+
+
+def batch_clips(lengths: list[int], start: int, end: int, seed: int = 0) -> list[np.ndarray]:
+    """Clips [start, end) of a universal-audio batch (speech-like on even global indices,
+    music-like on odd ones; seed per clip = seed + global index), so each rank synthesises only
+    its own shard of the global list."""
+    return [(speech_like if i % 2 == 0 else music_like)(lengths[i], seed + i) for i in range(start, end)]

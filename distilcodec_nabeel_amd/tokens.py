@@ -2,8 +2,10 @@
 
 Restates `DistilCodec.construct_audio_code` (distilcodec/distil_codec.py:200-265) and
 `DistilCodec.audio_tokenize` (:532-543): code n of group g / residual r maps to
-`{'content': '<|g{g}r{r}_{n+offset}|>', 'absolute_token_id': n + offset, 'in_codebook_id': n}`,
-offsets accumulate over codebooks, followed by 8 special audio tokens whose ids 5-7 carry the
+`{'content': '<|g{g}r{r}_{n+offset}|>', 'absolute_token_id': n + offset, 'in_codebook_id': n}`.
+The offset advances by one codebook size per GROUP, not per (group, residual): in the reference the
+`code_index_diff += codebook_size` sits after the residual loop (:219), so the residual codebooks of
+one group share an id range (reproduced as is).  The table ends with by 8 special audio tokens whose ids 5-7 carry the
 reference's +7/+8/+9 absolute ids (kept verbatim, :253-262).
 """
 from __future__ import annotations
@@ -28,7 +30,7 @@ def construct_audio_code(n_groups: int, n_residual: int, codebook_size: int, tok
             codes = {str(n): {"content": f"<|g{g}r{r}_{n + diff}|>", "absolute_token_id": n + diff, "in_codebook_id": n}
                      for n in range(codebook_size)}
             table[f"g{g}r{r}"] = {"codebook_size": codebook_size, "audio_code_token": codes}
-            diff += codebook_size
+        diff += codebook_size  # once per group (distil_codec.py:219)
     table["special_audio_tokens"] = {
         str(diff + i): {"content": c, "description": d, "absolute_token_id": diff + a}
         for i, (c, d, a) in enumerate(_SPECIAL)

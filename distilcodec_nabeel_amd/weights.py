@@ -56,9 +56,39 @@ def _wn(sd, seed, prefix, shape, std, bias_std=0.02, bias=True):
         sd[f"{prefix}.bias"] = _normal(seed, prefix + ".bias", (out_ch,), bias_std)
 
 
+PARTS = ("encoder", "quantizer", "generator")
+
+
 def synthetic_state_dict(cfg: dict, seed: int = 1234, with_generator: bool = True) -> dict:
     """Deterministic reference-format checkpoint `{encoder, quantizer, generator}` (numpy fp32)."""
-    enc_cfg, q_cfg, d_cfg = cfg["encoder"], cfg["quantizer"], cfg["decoder"]
+    return {"encoder": synthetic_encoder(cfg, seed), "quantizer": synthetic_quantizer(cfg, seed),
+            "generator": synthetic_generator(cfg, seed) if with_generator else {}}
+
+
+class LazyState(dict):
+    """`{part: state dict}` that synthesises a part (the same tensors synthetic_state_dict gives)
+    only when it is first read.  `DistilCodec.from_pretrained` assigns the checkpoint's parts before
+    anything reads them, so it never builds the 1.2 GB it replaces (the generator stays synthetic,
+    i.e. at its "initial weights", unless `use_generator`)."""
+
+    def __init__(self, cfg: dict, seed: int = 1234, parts=PARTS):
+        super().__init__()
+        self._cfg, self._seed, self._parts = cfg, seed, tuple(parts)
+
+    def __missing__(self, part):
+        if part not in self._parts:
+            raise KeyError(part)
+        v = {"encoder": synthetic_encoder, "quantizer": synthetic_quantizer, "generator": synthetic_generator}[part](
+            self._cfg, self._seed)
+        self[part] = v
+        return v
+
+    def materialised(self) -> tuple:
+        return tuple(k for k in PARTS if dict.__contains__(self, k))
+
+
+def synthetic_encoder(cfg: dict, seed: int = 1234) -> dict:
+    enc_cfg = cfg["encoder"]
     dims, depths, cin = enc_cfg["dims"], enc_cfg["depths"], enc_cfg["input_channels"]
     k = enc_cfg["kernel_size"]
 
@@ -78,7 +108,11 @@ def synthetic_state_dict(cfg: dict, seed: int = 1234, with_generator: bool = Tru
             _convnext(enc, seed, f"stages.{i}.{j}", dim, 0.3)
     enc["norm.weight"] = _normal(seed, "enc.norm.w", (dims[-1],), 0.1, 1.0)
     enc["norm.bias"] = _normal(seed, "enc.norm.b", (dims[-1],), 0.05)
+    return enc
 
+
+def synthetic_quantizer(cfg: dict, seed: int = 1234) -> dict:
+    q_cfg = cfg["quantizer"]
     D, CD, NC = q_cfg["input_dim"], q_cfg["codebook_dim"], q_cfg["codebook_size"]
     qd = {}
     qd["downsample.0.0.weight"] = _normal(seed, "q.down.w", (D, D, 1), 1.0 / np.sqrt(D))
@@ -93,22 +127,25 @@ def synthetic_state_dict(cfg: dict, seed: int = 1234, with_generator: bool = Tru
     qd["grvq.rvqs.0.project_out.bias"] = _normal(seed, "q.pout.b", (D,), 0.05)
     qd["grvq.rvqs.0.layers.0._codebook.embed"] = _normal(seed, "q.codebook", (1, NC, CD), CODEBOOK_STD)
     qd["grvq.rvqs.0.layers.0._codebook.initted"] = np.ones((1,), np.float32)
+    return qd
 
+
+def synthetic_generator(cfg: dict, seed: int = 1234) -> dict:
+    d_cfg = cfg["decoder"]
     gen = {}
-    if with_generator:
-        ch = d_cfg["upsample_initial_channel"]
-        pre_k, post_k = d_cfg["pre_conv_kernel_size"], d_cfg["post_conv_kernel_size"]
-        _wn(gen, seed, "conv_pre", (ch, d_cfg["num_mels"], pre_k), 1.0 / np.sqrt(d_cfg["num_mels"] * pre_k))
-        for i, (u, kk) in enumerate(zip(d_cfg["upsample_rates"], d_cfg["upsample_kernel_sizes"])):
-            cin_i, cout_i = ch // (2 ** i), ch // (2 ** (i + 1))
-            # each output sample of a stride-u ConvTranspose sees cin*k/u taps
-            _wn(gen, seed, f"ups.{i}", (cin_i, cout_i, kk), 1.5 / np.sqrt(cin_i * kk / u))
-            for b, (rk, dils) in enumerate(zip(d_cfg["resblock_kernel_sizes"], d_cfg["resblock_dilation_sizes"])):
-                for c in range(len(dils)):
-                    _wn(gen, seed, f"resblocks.{i}.blocks.{b}.convs1.{c}", (cout_i, cout_i, rk), 1.5 / np.sqrt(cout_i * rk))
-                    _wn(gen, seed, f"resblocks.{i}.blocks.{b}.convs2.{c}", (cout_i, cout_i, rk), 0.5 / np.sqrt(cout_i * rk))
-        _wn(gen, seed, "conv_post", (1, ch // (2 ** len(d_cfg["upsample_rates"])), post_k), 1.0 / np.sqrt(32 * post_k))
-    return {"encoder": enc, "quantizer": qd, "generator": gen}
+    ch = d_cfg["upsample_initial_channel"]
+    pre_k, post_k = d_cfg["pre_conv_kernel_size"], d_cfg["post_conv_kernel_size"]
+    _wn(gen, seed, "conv_pre", (ch, d_cfg["num_mels"], pre_k), 1.0 / np.sqrt(d_cfg["num_mels"] * pre_k))
+    for i, (u, kk) in enumerate(zip(d_cfg["upsample_rates"], d_cfg["upsample_kernel_sizes"])):
+        cin_i, cout_i = ch // (2 ** i), ch // (2 ** (i + 1))
+        # each output sample of a stride-u ConvTranspose sees cin*k/u taps
+        _wn(gen, seed, f"ups.{i}", (cin_i, cout_i, kk), 1.5 / np.sqrt(cin_i * kk / u))
+        for b, (rk, dils) in enumerate(zip(d_cfg["resblock_kernel_sizes"], d_cfg["resblock_dilation_sizes"])):
+            for c in range(len(dils)):
+                _wn(gen, seed, f"resblocks.{i}.blocks.{b}.convs1.{c}", (cout_i, cout_i, rk), 1.5 / np.sqrt(cout_i * rk))
+                _wn(gen, seed, f"resblocks.{i}.blocks.{b}.convs2.{c}", (cout_i, cout_i, rk), 0.5 / np.sqrt(cout_i * rk))
+    _wn(gen, seed, "conv_post", (1, ch // (2 ** len(d_cfg["upsample_rates"])), post_k), 1.0 / np.sqrt(32 * post_k))
+    return gen
 
 
 def fold_weight_norm(g: np.ndarray, v: np.ndarray) -> np.ndarray:

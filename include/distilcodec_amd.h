@@ -72,6 +72,9 @@ void dcx_destroy(dcx_codec* h);
 const char* dcx_last_error(const dcx_codec* h);
 const char* dcx_status_string(int status);
 int dcx_abi_version(void);
+/* First 16 hex digits of the SHA-256 of the library's sources (csrc/*.cpp|hip|h, sorted, then this
+ * header), fixed at build time.  The Python loader recomputes it and refuses a stale library. */
+const char* dcx_build_id(void);
 
 /* Checkpoint ingestion (replaces load_state_dict in DistilCodec.from_pretrained, :77-97).
  * `name` is "<part>.<state-dict key>" with part in {encoder, quantizer, generator}, e.g.
@@ -110,8 +113,10 @@ int dcx_vq_encode(dcx_codec* h, const float* feat, int32_t batch, int64_t frames
                   void* workspace, size_t ws_bytes, void* stream);
 
 /* DownsampleGRVQ.decode (grfvq.py:141-146): codes [B][T] int32 -> z [B][T][vq_dim].
- * Codes outside [0, codebook_size) are clamped to 0 and counted into *n_invalid (device int,
- * may be NULL); the reference passes them to the gather unchecked (distil_codec.py:584-586). */
+ * Negative codes in [-codebook_size, 0) wrap to code + codebook_size, like the torch indexing of
+ * the reference's gather (distil_codec.py:584-586, residual_vq.py:123).  Codes still outside
+ * [0, codebook_size) read row 0 and are counted into *n_invalid (device int, may be NULL); the
+ * Python surface raises IndexError for them before calling, as torch indexing would. */
 int dcx_vq_decode(dcx_codec* h, const int32_t* codes, int32_t batch, int64_t frames, float* z,
                   int32_t* n_invalid, void* workspace, size_t ws_bytes, void* stream);
 

@@ -4,11 +4,13 @@ Tolerances (fp32 path, identical inputs per stage):
   mel: max |log-mel diff| < 2e-3 and mean < 2e-5 (direct fp32 DFT vs pocketfft FFT)
   encoder / VQ features / quantized: max relative error < 2e-4
   codes: exact on decisive frames (fp64 relative top-2 gap > 1e-4), >= 97 % exact overall
-  waveform: SNR >= 80 dB vs the reference given identical codes
+  waveform: SNR >= 80 dB vs the reference, always (tests/_parity.py: when a non-decisive code
+    differs, the reference's codes are decoded on the GPU and held to the same bound)
 """
 import numpy as np
 import pytest
 import torch
+from _parity import check_codes, check_wave
 
 pytestmark = pytest.mark.gpu
 
@@ -65,8 +67,9 @@ def test_vq_encode_on_reference_features(eng, golden, state):
 
     emb = R.codebook(state["quantizer"])
     assert np.array_equal(fup.cpu().numpy(), emb[torch.from_numpy(codes).long()].numpy())
-    if (codes == g["codes"]).all():
-        assert _rel(q.transpose(1, 2), g["quantized"]) < 2e-4
+    # `quantized` unconditionally: from our codes when they all match, else decode the reference's
+    qz = q if (codes == g["codes"]).all() else eng.vq_decode(torch.from_numpy(g["codes"]))
+    assert _rel(qz.transpose(1, 2), g["quantized"]) < 2e-4
 
 
 def test_vq_decode(eng, golden):
@@ -89,10 +92,5 @@ def test_generator(eng, golden):
 def test_encode_decode_end_to_end(eng, golden, name):
     g = golden[name]
     codes, wav = eng.encode_decode(torch.from_numpy(g["audio"]))
-    codes = codes.cpu().numpy()
-    dec = _decisive(g)
-    assert np.array_equal(codes[dec], g["codes"][dec])
-    match = (codes == g["codes"]).mean()
-    assert match >= 0.97, match
-    if match == 1.0:
-        assert _snr(wav, g["wav"]) >= 80
+    check_codes(codes, g["codes"], _decisive(g))
+    check_wave(eng, codes, g["codes"], wav, g["wav"], 80)

@@ -1,5 +1,9 @@
-"""Multi-process clip sharding (world_size 2, gloo, CPU): every rank pads to the GLOBAL max length
-and the gathered codes equal a single-process run."""
+"""Multi-process clip sharding (world_size 2, gloo, CPU) with the reference's algorithm: each rank
+runs the CPU oracle (mel -> encoder -> GRFVQ search, oracle/reference_cpu.py) on its shard padded to
+the GLOBAL maximum, and the gathered codes equal a single-process run of the whole batch
+(pad-to-batch-max, distil_codec.py:133-136).  The same harness shows why every
+rank pads globally: padding a shard to its own maximum changes the codes of its longest clip.
+The GPU engine version of this test is tests/test_gpu_sharding.py."""
 import os
 import socket
 
@@ -11,15 +15,33 @@ import torch.multiprocessing as mp
 
 from distilcodec_nabeel_amd import sharding
 
+LENGTHS = [9000, 4000, 6500, 3001, 7777]
 
-def _fake_codes(padded: np.ndarray) -> torch.Tensor:
-    """Stand-in for the device path with the same batch dependence: frame energy depends on the
-    padded length, so a wrong global max changes the result."""
-    n = padded.shape[1]
-    T = (n + 768 - 1024) // 256 + 1
-    x = np.pad(padded, ((0, 0), (384, 384)), mode="reflect")
-    e = np.stack([np.abs(x[:, t * 256: t * 256 + 1024]).sum(1) for t in range(T)], 1)
-    return torch.from_numpy((e * 1e4).astype(np.int64) % 32768).to(torch.int32)
+
+def _state(cfg):
+    from distilcodec_nabeel_amd import weights
+
+    return {"encoder": weights.synthetic_encoder(cfg, 1234), "quantizer": weights.synthetic_quantizer(cfg, 1234)}
+
+
+def _oracle_codes(padded: np.ndarray, state, cfg) -> torch.Tensor:
+    """Codes of each padded clip, one clip at a time (the CPU library's result then depends on the
+    clip and its padding only, not on how clips are grouped)."""
+    from oracle import reference_cpu as R
+
+    out = []
+    with torch.no_grad():
+        for row in padded:
+            mel = R.log_mel(torch.from_numpy(row)[None])
+            feat = R.encoder(mel, state["encoder"], tuple(cfg["encoder"]["depths"]))
+            out.append(R.vq_forward(feat, state["quantizer"])["codes"][0, 0, :, 0])
+    return torch.stack(out).to(torch.int32) if out else torch.empty(0, 0, dtype=torch.int32)
+
+
+def _clips():
+    from distilcodec_nabeel_amd import synth
+
+    return synth.batch_clips(LENGTHS, 0, len(LENGTHS), seed=11)
 
 
 def _free_port():
@@ -32,31 +54,84 @@ def _free_port():
 
 def _worker(rank, world, port, clips, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    from distilcodec_nabeel_amd import config
+
+    cfg = config.default_config()
+    state = _state(cfg)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out = sharding.encode_sharded(_fake_codes, clips, rank, world, gather=True)
+        out = sharding.encode_sharded(lambda p: _oracle_codes(p, state, cfg), clips, rank, world, gather=True)
         q.put((rank, out.numpy()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_clips", [5, 2])
-def test_gloo_world2_matches_single_process(n_clips):
-    r = np.random.default_rng(1)
-    clips = [r.standard_normal(int(r.integers(3000, 9000))).astype(np.float32) * 0.1 for _ in range(n_clips)]
-    expect = _fake_codes(sharding.pad_to_global(clips, max(len(c) for c in clips))).numpy()
+@pytest.fixture(scope="module")
+def expect(cfg):
+    torch.set_num_threads(4)
+    clips = _clips()
+    state = _state(cfg)
+    full = _oracle_codes(sharding.pad_to_global(clips, max(LENGTHS)), state, cfg).numpy()
+    # rank 1's shard (clips 3, 4) padded to its own maximum instead of the global one
+    s, e = sharding.shard_bounds(len(clips), 1, 2)
+    own = _oracle_codes(sharding.pad_to_global(clips[s:e], max(LENGTHS[s:e])), state, cfg).numpy()
+    return full, own, (s, e)
+
+
+def test_gloo_world2_oracle_matches_single_process(expect):
+    full, _, _ = expect
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(rk, 2, port, clips, q)) for rk in range(2)]
+    procs = [ctx.Process(target=_worker, args=(rk, 2, port, _clips(), q)) for rk in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(2))
+    res = dict(q.get(timeout=300) for _ in range(2))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     for rk in range(2):
-        assert np.array_equal(res[rk], expect)
+        assert res[rk].shape == full.shape
+        assert np.array_equal(res[rk], full)
+
+
+def test_global_padding_is_what_matters(expect):
+    """Clip 4 (7777 samples) is the longest of rank 1's shard: with the shard padded to its own
+    maximum, its last frames see the STFT's reflect padding instead of the zeros the whole batch
+    gives it, and its codes near the end change (the encoder's receptive field spreads the
+    difference over ~60 frames, streaming.receptive_field)."""
+    full, own, (s, e) = expect
+    n = own.shape[1]
+    j = int(np.argmax(LENGTHS[s:e]))
+    assert not np.array_equal(full[s + j, :n], own[j])
+
+
+def test_gather_rows_uneven_shards():
+    """gather_rows reassembles unequal shards in rank order (world 3 over 7 rows, gloo)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(rk, 3, port, q)) for rk in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rk in range(3):
+        assert np.array_equal(res[rk], np.arange(7 * 2).reshape(7, 2))
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, e = sharding.shard_bounds(7, rank, world)
+        local = torch.arange(s * 2, e * 2).reshape(e - s, 2)
+        q.put((rank, sharding.gather_rows(local, 7, world).numpy()))
+    finally:
+        dist.destroy_process_group()
 
 
 def test_shard_bounds_cover_everything():
@@ -67,3 +142,14 @@ def test_shard_bounds_cover_everything():
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             sizes = [e - s for s, e in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+def test_ragged_batch_is_deterministic_and_shardable():
+    from distilcodec_nabeel_amd import synth
+
+    lens = synth.ragged_lengths(16, 7, 240000, 216000)
+    assert lens[0] == 240000 and min(lens) >= 216000 and lens == synth.ragged_lengths(16, 7, 240000, 216000)
+    parts = [synth.batch_clips([1000] * 6, *sharding.shard_bounds(6, r, 3), seed=2) for r in range(3)]
+    whole = synth.batch_clips([1000] * 6, 0, 6, seed=2)
+    assert all(np.array_equal(a, b) for a, b in zip(sum(parts, []), whole))
+    assert all(np.array_equal(a, b) for a, b in zip(whole, synth.clips(6, 1000, seed=2, kind="mix")))
