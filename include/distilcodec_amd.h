@@ -72,8 +72,8 @@ void dcx_destroy(dcx_codec* h);
 const char* dcx_last_error(const dcx_codec* h);
 const char* dcx_status_string(int status);
 int dcx_abi_version(void);
-/* First 16 hex digits of the SHA-256 of the library's sources (csrc/*.cpp|hip|h, sorted, then this
- * header), fixed at build time.  The Python loader recomputes it and refuses a stale library. */
+/* First 16 hex digits of the SHA-256 of the library's sources (the .cpp/.hip/.h files under csrc,
+ * sorted, then this header), fixed at build time.  The Python loader recomputes it and refuses a stale library. */
 const char* dcx_build_id(void);
 
 /* Checkpoint ingestion (replaces load_state_dict in DistilCodec.from_pretrained, :77-97).
