@@ -10,6 +10,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -106,6 +107,9 @@ struct dcx_codec {
   unsigned short* codebook6 = nullptr;
   unsigned short* ptable6 = nullptr;  // decode table as activation planes (x6 mode gathers)
   int gemm_mode = DCX_GEMM_X6;
+  // fused ResBlock pairs for the C = 32 / 64 generator stages (conv_res_pair); DCX_NO_RESPAIR=1 at
+  // dcx_create keeps the per-conv launches (A/B comparisons)
+  bool res_pair = true;
 
   ConvW conv_pre;
   ConvW ups[8];
@@ -817,6 +821,24 @@ int stage_vq_decode(dcx_codec* h, const int32_t* codes, int B, int T, Act z, int
   return DCX_OK;
 }
 
+// The fused pair kernel serves a stage when its ResBlock convs are C = 32 / 64 in x6 arithmetic with
+// odd kernels, c2 reach <= 8 and c1 reach <= 32 rows, and biases (launch_res_pair checks again).
+bool res_pair_ok(const dcx_codec* h, int stage) {
+  if (!h->res_pair || h->gemm_mode != DCX_GEMM_X6) return false;
+  const dcx_config& c = h->cfg;
+  for (int rb = 0; rb < c.n_res; ++rb)
+    for (int ci = 0; ci < 3; ++ci)
+      for (int j = 0; j < 2; ++j) {
+        const ConvW& w = h->res[stage][rb][ci][j];
+        const int hk = (w.taps - 1) / 2;
+        if ((w.cout != 32 && w.cout != 64) || w.cin != w.cout || !w.w6 || !w.b || w.taps % 2 == 0 || hk > 8 ||
+            w.phases != 1 || w.in_step < 1 || hk * w.in_step > 32 || w.in_base[0] != -hk * w.in_step ||
+            (j == 1 && w.in_step != 1))
+          return false;
+      }
+  return true;
+}
+
 int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hipStream_t s) {
   const dcx_config& c = h->cfg;
   RUN(ensure_planes(h, z, (long long)B * T, c.vq_dim, ws, s));
@@ -870,6 +892,48 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
       RUN(run_conv(h, up, cc, s));
     }
     const bool last_stage = i == c.n_ups - 1;
+    if (silu_on_load && res_pair_ok(h, i)) {
+      // fused pairs: X -> R[rb] -> Tb[rb] (as fp32) -> silu(ParallelBlock mean)
+      float* Ra[NR];
+      float* Rb[NR];
+      for (int rb = 0; rb < c.n_res; ++rb) {
+        Ra[rb] = R[rb];
+        Rb[rb] = Tb[rb].f ? Tb[rb].f : reinterpret_cast<float*>(Tb[rb].p);
+      }
+      float* out = last_stage ? Mx : in_form(S, h->ups[i + 1]).f;
+      for (int ci = 0; ci < 3; ++ci) {
+        dcx::ResPairParams rp{};
+        double fl = 0, by = 0;
+        for (int rb = 0; rb < c.n_res; ++rb) {
+          const ConvW& w1 = h->res[i][rb][ci][0];
+          const ConvW& w2 = h->res[i][rb][ci][1];
+          rp.src[rb] = ci == 0 ? X : (ci == 1 ? Ra[rb] : Rb[rb]);
+          rp.dst[rb] = ci == 0 ? Ra[rb] : (ci == 1 ? Rb[rb] : nullptr);
+          rp.w1[rb] = w1.w6;
+          rp.w2[rb] = w2.w6;
+          rp.b1[rb] = w1.b;
+          rp.b2[rb] = w2.b;
+          rp.taps[rb] = w1.taps;
+          rp.dil[rb] = w1.in_step;
+          ConvCall cc = framed(Act{X, nullptr}, B, Lo, Co);
+          fl += conv_flops(w1, cc) + conv_flops(w2, cc);
+          by += 8.0 * B * Lo * Co;
+        }
+        rp.nmem = c.n_res;
+        rp.mean_out = ci == 2 ? out : nullptr;
+        rp.bstride = (long long)Lo * Co;
+        rp.L = Lo;
+        rp.batch = B;
+        rp.C = Co;
+        ProfScope ps(h, s);
+        const char* kname = "conv_res_pair";
+        HIPCHK(h, dcx::launch_res_pair(rp, s, &kname));
+        ps.done(kname, fl, by);
+      }
+      C = Co;
+      L = Lo;
+      continue;
+    }
     for (int ci = 0; ci < 3; ++ci) {
       const ConvW* w1[NR];
       ConvCall c1[NR];
@@ -1030,6 +1094,8 @@ int dcx_create(const dcx_config* cfg, dcx_codec** out) {
   if (!h) return DCX_ERR_OOM;
   h->cfg = c;
   hipGetDevice(&h->device);
+  const char* nrp = std::getenv("DCX_NO_RESPAIR");
+  h->res_pair = !(nrp && nrp[0] == '1');
   *out = h;
   return DCX_OK;
 }

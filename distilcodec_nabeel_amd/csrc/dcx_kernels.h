@@ -70,12 +70,32 @@ struct ConvGroup {
   int tiles_per_clip[kMaxGroup];
 };
 
+// One pair (c1 dilated, c2 undilated) of each ResBlock1 of a small-channel ParallelBlock (C = 32 / 64,
+// x6 arithmetic), fused: silu(c1) stays in LDS (dcx_resblock.hip).  Member m reads state src[m]
+// ([clip][L][C] fp32) and writes src[m] + c2(silu(c1(silu(src[m])))) to dst[m] (dst != src: the
+// tap halo makes in-place updates race), or, with mean_out set, silu of the mean over the members
+// (ParralelBlock, ResBlock order) to mean_out.  Weights: the x6 planes packing of ConvParams::w6.
+struct ResPairParams {
+  const float* src[kMaxGroup];
+  float* dst[kMaxGroup];
+  const unsigned short* w1[kMaxGroup];
+  const unsigned short* w2[kMaxGroup];
+  const float* b1[kMaxGroup];
+  const float* b2[kMaxGroup];
+  int taps[kMaxGroup], dil[kMaxGroup];  // c1 taps (odd, (taps - 1) / 2 <= 8) and dilation (reach <= 32)
+  int nmem;
+  float* mean_out;
+  long long bstride;  // elements between clips
+  int L, batch, C;
+};
+
 // Launchers (all stream-ordered, no allocation).  Return hipError_t of the launch.
 hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname);
 // n <= kMaxGroup independent single-phase convs with one column tiling as one launch of the
 // LDS-DMA 16x16x32 kernel; hipErrorNotSupported when they do not all qualify (the caller then
 // launches them one by one, which gives the same bits).
 hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t s, const char** kname);
+hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** kname);
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname);
 int vq_argmin_ntiles(int ncodes);
 // per-row partial count of the x6-mode prefilter (launch_vq_prefilter)

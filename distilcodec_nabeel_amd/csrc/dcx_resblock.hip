@@ -1,0 +1,350 @@
+// Fused ResBlock1 pairs for the small-channel generator stages (C = 32 and 64).
+//
+// ResBlock1 (convnext_utils.py:106-113) runs three pairs
+//     xt = c2(silu(c1(silu(x))));  x = xt + x
+// with c1 dilated (k, d) and c2 undilated (k, 1); ParralelBlock (:137-138) averages three such
+// ResBlocks (k = 3 / 7 / 11).  At C = 32 / 64 each conv has K = k * C <= 704, so one conv per launch
+// (conv_gemm_x6w4f / x6pf) spent its time staging and splitting its fp32 input and round-tripping
+// silu(c1) through HBM rather than in MFMAs (0.30 / 0.47 MFMA busy, 7 SALU + 8 VALU per MFMA).
+//
+// conv_res_pair runs one pair of all three ResBlocks per launch.  A workgroup owns R output rows of
+// one clip and, for each ResBlock in turn:
+//   1. S image: silu(state) as x6 planes in LDS, rows [r0 - 8 - 32, r0 + R + 8 + 32) (zero outside
+//      the clip = the conv's zero padding), prefetched into registers during the previous c2;
+//   2. c1 over the R + 16 rows [r0 - 8, r0 + R + 8) (the c2 halo, (k - 1) / 2 <= 8);
+//   3. T image: silu(c1 + b1) planes written over S (zero outside the clip);
+//   4. c2 over the R output rows, epilogue state + c2 + b2 to the next state buffer (or, for the
+//      last pair, into the ParallelBlock mean, kept in registers across the three ResBlocks in
+//      ResBlock order: m = v0; m += v1; m = (m + v2) / 3, then silu(mean) to the next ConvT input).
+// The halo makes in-place updates race, so each pair writes a buffer other than the one it reads.
+//
+// Arithmetic: the x6 products of conv_gemm_x6dq (v_mfma_f32_16x16x32_bf16, the K dimension split
+// into (term, channel)), with the weights as the A operand and the activations as B, so each lane's
+// accumulator holds 4 consecutive channels of one time row: T-image writes are 8-byte plane stores
+// and epilogue loads / stores are 16-byte fp32 accesses.
+//   W{h',m'} . X{h,m} = hh' + mm',  W{h',m'} . X{m,h} = mh' + hm',  W{h',l'} . X{l,h} = lh' + hl'.
+// Weights stream through a 2-slot LDS ring, one tap (C * C * 6 bytes) per step, prefetched one
+// step ahead into registers; the step sequence runs on across convs, ResBlocks and tiles.
+// LDS images: 16-row blocks, [row >> 4][chunk][piece 6][row & 15][16 B] (piece = half * 3 +
+// plane), so every ds_read_b128 of 16 consecutive rows of one piece is conflict-free at any tap
+// offset, and the weight slot is the global tap slice [chunk][Cout][96 B] copied as is.
+#include <algorithm>
+
+#include "dcx_kernels.h"
+#include "dcx_planes.h"
+
+namespace dcx {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float rp_silu(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
+// barrier that leaves global loads in flight (only LDS traffic is drained)
+__device__ __forceinline__ void rp_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+typedef __attribute__((address_space(3))) void* rp_lds_t;
+// retire this wave's weight pieces: all but the n youngest vector-memory ops (the prefetch loads
+// issued after the pieces) done
+__device__ __forceinline__ void rp_wait(int n) {
+#define RP_W(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+  switch (n) {
+    RP_W(8) RP_W(10) RP_W(14) RP_W(16) RP_W(18) RP_W(24) RP_W(26)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+#undef RP_W
+}
+
+template <int C>
+struct RpGeom {
+  static constexpr int R = C == 32 ? 496 : 176;  // output rows per tile
+  static constexpr int M1 = R + 16;              // c1 rows: [r0 - 8, r0 + R + 8)
+  static constexpr int H1 = 32;                  // largest c1 reach (k - 1) / 2 * d
+  static constexpr int NS = M1 + 2 * H1;         // S image rows
+  static constexpr int NCH = C / 16;             // K16 chunks per tap
+  static constexpr int WC = C / 32, WR = 8 / WC; // waves: WR row groups x WC column halves (32 ch)
+  static constexpr int NB1 = M1 / 16, RB1 = NB1 / WR;
+  static constexpr int NB2 = R / 16, RB2 = (NB2 + WR - 1) / WR;
+  static constexpr int BLK = NCH * 1536;         // bytes per 16-row block of an image
+  static constexpr int IMG = NS / 16 * BLK;      // S image bytes (T reuses its start)
+  static constexpr int WSLOT = C * C * 6;        // one tap of weights
+  static constexpr int G8 = C / 8;               // 8-channel groups per row
+  static constexpr int NIT = (NS * G8 + 511) / 512;
+  static constexpr int WP = WSLOT / 1024, WPW = (WP + 7) / 8;  // DMA pieces per tap, per wave
+  static_assert(NB1 % WR == 0 && RB1 == RB2, "row blocks per wave");
+  static_assert(IMG + 2 * WSLOT <= 160 * 1024, "LDS");
+};
+
+}  // namespace
+
+template <int C, bool MEAN>
+__global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
+  using G = RpGeom<C>;
+  constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB1, BLK = G::BLK, IMG = G::IMG;
+  constexpr int WSLOT = G::WSLOT, G8 = G::G8, NIT = G::NIT, WP = G::WP, WPW = G::WPW, NS = G::NS;
+  __shared__ __attribute__((aligned(16))) char lds[IMG + 2 * WSLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wc = wave % G::WC, wr = wave / G::WC;
+  const int l15 = lane & 15, hf = (lane >> 4) & 1, t = lane >> 5;
+  const int L = p.L, nmem = p.nmem;
+  const int ntl = (L + R - 1) / R;
+  const int total = ntl * p.batch;
+
+  // ---- weight ring: LDS-DMA of one tap slice (lane-linear 1 KiB pieces, no staging registers) ----
+  auto issue_w = [&](const unsigned short* w, int slot) {
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)w, 0, WSLOT, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < WPW; ++k) {
+      const int piece = wave + 8 * k;
+      if (WP % 8 == 0 || piece < WP)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (rp_lds_t)(lds + IMG + slot * WSLOT + piece * 1024), 16,
+                                                 piece * 1024 + lane * 16, 0, 0, 0);
+    }
+    asm volatile("" ::: "memory");  // later loads stay younger than the pieces (rp_wait counts them)
+  };
+  auto wtap = [&](int m, int conv, int j) -> const unsigned short* {
+    return (conv ? p.w2[m] : p.w1[m]) + (long long)j * (WSLOT / 2);
+  };
+
+  // ---- S image fill: state rows -> registers (issue) -> silu, planes, LDS (commit) ----
+  f32x4 pf[NIT][2];
+  auto issue_fill = [&](const float* src, int r0) {
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int it = min(tid + 512 * k, NS * G8 - 1);  // unconditional (rp_wait counts the loads)
+      const int s = ((it >> 3) / G8) * 8 + (it & 7), g8 = (it >> 3) % G8;
+      const int a = min(max(r0 - 8 - G::H1 + s, 0), L - 1);
+      const f32x4* q = reinterpret_cast<const f32x4*>(src + (long long)a * C + g8 * 8);
+      pf[k][0] = q[0];
+      pf[k][1] = q[1];
+    }
+  };
+  auto commit_fill = [&](int r0) {
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int it = tid + 512 * k;
+      if (!(NIT * 512 == NS * G8 || it < NS * G8)) continue;
+      const int s = ((it >> 3) / G8) * 8 + (it & 7), g8 = (it >> 3) % G8;
+      const int a = r0 - 8 - G::H1 + s;
+      const bool ok = a >= 0 && a < L;
+      s16x8 hv, mv, lv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = ok ? rp_silu(pf[k][e >> 2][e & 3]) : 0.f;
+        unsigned short h, m, l;
+        split3(v, h, m, l);
+        hv[e] = (short)h;
+        mv[e] = (short)m;
+        lv[e] = (short)l;
+      }
+      char* d = lds + (s >> 4) * BLK + (g8 >> 1) * 1536 + (g8 & 1) * 768 + (s & 15) * 16;
+      *reinterpret_cast<s16x8*>(d) = hv;
+      *reinterpret_cast<s16x8*>(d + 256) = mv;
+      *reinterpret_cast<s16x8*>(d + 512) = lv;
+    }
+  };
+
+  // ---- one step: every chunk of one tap, rows of this wave, its 2 column blocks ----
+  const int soX0 = (hf * 3 + t) * 256, soX1 = (hf * 3 + (t ? 0 : 1)) * 256, soX2 = (hf * 3 + (t ? 0 : 2)) * 256;
+  auto mfma_step = [&](f32x4 (&acc)[RB][2], int slot, int rowoff, int nrb) {
+    const char* wb = lds + IMG + slot * WSLOT;
+    s16x8 wf[NCH][2][2];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const char* w = wb + (ch * C + (2 * wc + cb) * 16 + l15) * 96 + hf * 48;
+        wf[ch][cb][0] = *reinterpret_cast<const s16x8*>(w + t * 16);        // {h', m'}
+        wf[ch][cb][1] = *reinterpret_cast<const s16x8*>(w + (t ? 32 : 0));  // {h', l'}
+      }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      if (i >= nrb) break;
+      const int sr = (wr + WR * i) * 16 + l15 + rowoff;
+      const char* xr = lds + (sr >> 4) * BLK + (sr & 15) * 16;
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const s16x8 x2 = *reinterpret_cast<const s16x8*>(xr + ch * 1536 + soX2);
+        const s16x8 x1 = *reinterpret_cast<const s16x8*>(xr + ch * 1536 + soX1);
+        const s16x8 x0 = *reinterpret_cast<const s16x8*>(xr + ch * 1536 + soX0);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][1]),
+                                                               __builtin_bit_cast(bf16x8, x2), acc[i][cb], 0, 0, 0);
+          acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][0]),
+                                                               __builtin_bit_cast(bf16x8, x1), acc[i][cb], 0, 0, 0);
+          acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][0]),
+                                                               __builtin_bit_cast(bf16x8, x0), acc[i][cb], 0, 0, 0);
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // rows of c2 this wave owns
+  const int nrb2 = min(RB, (G::NB2 - wr + WR - 1) / WR);
+  int tile = blockIdx.x;
+  if (tile >= total) return;  // whole workgroup, before any barrier
+  int b = tile / ntl, r0 = (tile - b * ntl) * R;
+  // prologue: first ResBlock's S image and first weight tap
+  issue_w(wtap(0, 0, 0), 0);
+  issue_fill(p.src[0] + (long long)b * p.bstride, r0);
+  commit_fill(r0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  rp_barrier();
+  int slot = 0;
+  f32x4 macc[MEAN ? RB : 1][2];
+  for (;;) {
+    const int next_tile = tile + gridDim.x;
+    const bool more = next_tile < total;
+    const int nb = more ? next_tile / ntl : 0, nr0 = more ? (next_tile - nb * ntl) * R : 0;
+    for (int m = 0; m < nmem; ++m) {
+      const int k = p.taps[m], hk = (k - 1) >> 1, d = p.dil[m];
+      const long long cb0 = (long long)b * p.bstride;
+      f32x4 acc[RB][2];
+      // ---- c1 over rows [r0 - 8, r0 + R + 8) from the S image
+#pragma unroll
+      for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < k; ++j) {
+        issue_w(j + 1 < k ? wtap(m, 0, j + 1) : wtap(m, 1, 0), slot ^ 1);
+        mfma_step(acc, slot, G::H1 + (j - hk) * d, RB);
+        rp_wait(0);
+        rp_barrier();
+        slot ^= 1;
+      }
+      // ---- T image: silu(c1 + b1) planes over the S image (zero outside the clip)
+      {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+          const f32x4 bias = *reinterpret_cast<const f32x4*>(p.b1[m] + c0);
+#pragma unroll
+          for (int i = 0; i < RB; ++i) {
+            const int ir = (wr + WR * i) * 16 + l15, a = r0 - 8 + ir;
+            const bool ok = a >= 0 && a < L;
+            s16x4 hv, mv, lv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = ok ? rp_silu(acc[i][cb][e] + bias[e]) : 0.f;
+              unsigned short h, mm, l;
+              split3(v, h, mm, l);
+              hv[e] = (short)h;
+              mv[e] = (short)mm;
+              lv[e] = (short)l;
+            }
+            char* dst = lds + (ir >> 4) * BLK + (c0 >> 4) * 1536 + ((c0 >> 3) & 1) * 768 + (ir & 15) * 16 + (c0 & 7) * 2;
+            *reinterpret_cast<s16x4*>(dst) = hv;
+            *reinterpret_cast<s16x4*>(dst + 256) = mv;
+            *reinterpret_cast<s16x4*>(dst + 512) = lv;
+          }
+        }
+      }
+      rp_barrier();
+      // ---- c2 over rows [r0, r0 + R) from the T image; residual rows prefetched
+#pragma unroll
+      for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool last_m = m + 1 == nmem;
+      const bool has_next = !last_m || more;
+      // the next S image (this tile's next ResBlock, or the next tile's first) and the residual
+      // rows are loaded two steps before the end of c2 (latency hidden, registers held briefly)
+      const int jpf = k > 2 ? k - 2 : 0;
+      f32x4 res[RB][2];
+      for (int j = 0; j < k; ++j) {
+        if (j + 1 < k) issue_w(wtap(m, 1, j + 1), slot ^ 1);
+        else if (has_next) issue_w(wtap(last_m ? 0 : m + 1, 0, 0), slot ^ 1);
+        int younger = 0;
+        if (j == jpf) {
+          younger = 2 * RB + (has_next ? 2 * NIT : 0);
+          if (has_next) {
+            if (!last_m) issue_fill(p.src[m + 1] + cb0, r0);
+            else issue_fill(p.src[0] + (long long)nb * p.bstride, nr0);
+          }
+#pragma unroll
+          for (int i = 0; i < RB; ++i) {
+            const int q = min(r0 + (wr + WR * i) * 16 + l15, L - 1);
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+              const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+              res[i][cb] = *reinterpret_cast<const f32x4*>(p.src[m] + cb0 + (long long)q * C + c0);
+            }
+          }
+        }
+        mfma_step(acc, slot, 8 + j - hk, nrb2);
+        rp_wait(younger);
+        rp_barrier();
+        slot ^= 1;
+      }
+      // ---- epilogue: state + c2 + b2 (rows past the clip end are dropped)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(p.b2[m] + c0);
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          if (i >= nrb2) break;
+          const int q = r0 + (wr + WR * i) * 16 + l15;
+          const f32x4 v = res[i][cb] + (acc[i][cb] + bias);
+          if constexpr (!MEAN) {
+            if (q < L) *reinterpret_cast<f32x4*>(p.dst[m] + cb0 + (long long)q * C + c0) = v;
+          } else if (m == 0) {
+            macc[i][cb] = v;
+          } else if (!last_m) {
+            macc[i][cb] = macc[i][cb] + v;
+          } else {
+            const f32x4 mv = (macc[i][cb] + v) / 3.0f;
+            f32x4 sv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sv[e] = rp_silu(mv[e]);
+            if (q < L) *reinterpret_cast<f32x4*>(p.mean_out + cb0 + (long long)q * C + c0) = sv;
+          }
+        }
+      }
+      if (has_next) {
+        commit_fill(last_m ? nr0 : r0);
+        rp_barrier();
+      }
+    }
+    if (!more) break;
+    tile = next_tile;
+    b = nb;
+    r0 = nr0;
+  }
+}
+
+hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** kname) {
+  if (p.nmem < 1 || p.nmem > kMaxGroup || p.batch < 1 || p.L < 1 || (p.C != 32 && p.C != 64))
+    return hipErrorInvalidValue;
+  for (int m = 0; m < p.nmem; ++m) {
+    const int hk = (p.taps[m] - 1) / 2;
+    if (p.taps[m] < 1 || p.taps[m] % 2 == 0 || hk > 8 || p.dil[m] < 1 || hk * p.dil[m] > 32 || !p.src[m] ||
+        !p.w1[m] || !p.w2[m] || !p.b1[m] || !p.b2[m] || (!p.mean_out && !p.dst[m]))
+      return hipErrorInvalidValue;
+  }
+  const int R = p.C == 32 ? RpGeom<32>::R : RpGeom<64>::R;
+  const long long total = (long long)((p.L + R - 1) / R) * p.batch;
+  if (total > (1LL << 30)) return hipErrorInvalidValue;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      return hipErrorInvalidValue;
+  }
+  const unsigned grid = (unsigned)std::min<long long>(total, cus);  // one workgroup per CU (LDS)
+  if (p.C == 32) {
+    if (kname) *kname = p.mean_out ? "conv_res_pair<32,mean>" : "conv_res_pair<32>";
+    if (p.mean_out) hipLaunchKernelGGL((conv_res_pair<32, true>), dim3(grid), dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((conv_res_pair<32, false>), dim3(grid), dim3(512), 0, s, p);
+  } else {
+    if (kname) *kname = p.mean_out ? "conv_res_pair<64,mean>" : "conv_res_pair<64>";
+    if (p.mean_out) hipLaunchKernelGGL((conv_res_pair<64, true>), dim3(grid), dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((conv_res_pair<64, false>), dim3(grid), dim3(512), 0, s, p);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dcx
