@@ -57,6 +57,16 @@ __device__ __forceinline__ void rp_wait(int n) {
 #undef RP_W
 }
 
+#ifdef RP_DIAG_STAMPS
+// Diagnostic build only: shader-clock sums per phase of conv_res_pair (wave 0 of every workgroup):
+// [0] c1 steps, [1] T image, [2] c2 step 0 (with the prefetch issue), [3] c2 steps 1.., [4] epilogue,
+// [5] next S image, [6] member-tiles, [7] c1 steps counted, [8] c2 steps counted.
+__device__ unsigned long long g_rp_diag[32];  // [C == 64][16]
+#define RP_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define RP_T(v)
+#endif
+
 template <int C>
 struct RpGeom {
   static constexpr int R = C == 32 ? 496 : 176;  // output rows per tile
@@ -74,7 +84,7 @@ struct RpGeom {
   static constexpr int NIT = (NS * G8 + 511) / 512;
   static constexpr int WP = WSLOT / 1024, WPW = (WP + 7) / 8;  // DMA pieces per tap, per wave
   static_assert(NB1 % WR == 0 && RB1 == RB2, "row blocks per wave");
-  static_assert(IMG + 2 * WSLOT <= 160 * 1024, "LDS");
+  static_assert(IMG + 2 * WSLOT + 2 * kMaxGroup * C * 4 <= 160 * 1024, "LDS");
 };
 
 }  // namespace
@@ -84,7 +94,8 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
   using G = RpGeom<C>;
   constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB1, BLK = G::BLK, IMG = G::IMG;
   constexpr int WSLOT = G::WSLOT, G8 = G::G8, NIT = G::NIT, WP = G::WP, WPW = G::WPW, NS = G::NS;
-  __shared__ __attribute__((aligned(16))) char lds[IMG + 2 * WSLOT];
+  __shared__ __attribute__((aligned(16))) char lds[IMG + 2 * WSLOT + 2 * kMaxGroup * C * 4];
+  float* const bias_lds = reinterpret_cast<float*>(lds + IMG + 2 * WSLOT);  // [conv][member][C]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wc = wave % G::WC, wr = wave / G::WC;
@@ -123,6 +134,9 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
     }
   };
   auto commit_fill = [&](int r0) {
+#ifdef RP_DIAG_NOVALU
+    return;
+#endif
 #pragma unroll
     for (int k = 0; k < NIT; ++k) {
       const int it = tid + 512 * k;
@@ -133,9 +147,16 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
       s16x8 hv, mv, lv;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float v = ok ? rp_silu(pf[k][e >> 2][e & 3]) : 0.f;
+#ifdef RP_DIAG_RAW
+        const float v = ok ? pf[k][e >> 2][e & 3] : 0.f;
+        const unsigned u = __float_as_uint(v);
+        unsigned short h = u >> 16, m = u & 0xffff, l = h;
+#else
+        const float sv = rp_silu(pf[k][e >> 2][e & 3]);
+        const float v = ok ? sv : 0.f;
         unsigned short h, m, l;
         split3(v, h, m, l);
+#endif
         hv[e] = (short)h;
         mv[e] = (short)m;
         lv[e] = (short)l;
@@ -191,6 +212,10 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
   if (tile >= total) return;  // whole workgroup, before any barrier
   int b = tile / ntl, r0 = (tile - b * ntl) * R;
   // prologue: first ResBlock's S image and first weight tap
+  if (tid < 2 * nmem * C) {
+    const int conv = tid / (nmem * C), m = (tid / C) % nmem, c = tid % C;
+    bias_lds[(conv * kMaxGroup + m) * C + c] = (conv ? p.b2[m] : p.b1[m])[c];
+  }
   issue_w(wtap(0, 0, 0), 0);
   issue_fill(p.src[0] + (long long)b * p.bstride, r0);
   commit_fill(r0);
@@ -198,6 +223,9 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
   rp_barrier();
   int slot = 0;
   f32x4 macc[MEAN ? RB : 1][2];
+#ifdef RP_DIAG_STAMPS
+  unsigned long long dg[16] = {};
+#endif
   for (;;) {
     const int next_tile = tile + gridDim.x;
     const bool more = next_tile < total;
@@ -206,22 +234,37 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
       const int k = p.taps[m], hk = (k - 1) >> 1, d = p.dil[m];
       const long long cb0 = (long long)b * p.bstride;
       f32x4 acc[RB][2];
+      RP_T(ta);
       // ---- c1 over rows [r0 - 8, r0 + R + 8) from the S image
 #pragma unroll
       for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int j = 0; j < k; ++j) {
+        RP_T(s0);
         issue_w(j + 1 < k ? wtap(m, 0, j + 1) : wtap(m, 1, 0), slot ^ 1);
+        RP_T(s1);
         mfma_step(acc, slot, G::H1 + (j - hk) * d, RB);
+        RP_T(s2);
+#ifndef RP_DIAG_NOBAR
         rp_wait(0);
+        RP_T(s3);
         rp_barrier();
+#endif
+#ifdef RP_DIAG_STAMPS
+        {
+          RP_T(s4);
+          dg[9] += s1 - s0; dg[10] += s2 - s1; dg[11] += s3 - s2; dg[12] += s4 - s3;
+        }
+#endif
         slot ^= 1;
       }
+      RP_T(tb);
       // ---- T image: silu(c1 + b1) planes over the S image (zero outside the clip)
+#ifndef RP_DIAG_NOVALU
       {
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
           const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
-          const f32x4 bias = *reinterpret_cast<const f32x4*>(p.b1[m] + c0);
+          const f32x4 bias = *reinterpret_cast<const f32x4*>(bias_lds + m * C + c0);
 #pragma unroll
           for (int i = 0; i < RB; ++i) {
             const int ir = (wr + WR * i) * 16 + l15, a = r0 - 8 + ir;
@@ -229,9 +272,16 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
             s16x4 hv, mv, lv;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float v = ok ? rp_silu(acc[i][cb][e] + bias[e]) : 0.f;
+#ifdef RP_DIAG_RAW
+              const float v = ok ? acc[i][cb][e] + bias[e] : 0.f;
+              const unsigned u = __float_as_uint(v);
+              unsigned short h = u >> 16, mm = u & 0xffff, l = h;
+#else
+              const float sv = rp_silu(acc[i][cb][e] + bias[e]);
+              const float v = ok ? sv : 0.f;
               unsigned short h, mm, l;
               split3(v, h, mm, l);
+#endif
               hv[e] = (short)h;
               mv[e] = (short)mm;
               lv[e] = (short)l;
@@ -243,46 +293,64 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
           }
         }
       }
+#endif
       rp_barrier();
+      RP_T(tc);
       // ---- c2 over rows [r0, r0 + R) from the T image; residual rows prefetched
 #pragma unroll
       for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
       const bool last_m = m + 1 == nmem;
       const bool has_next = !last_m || more;
-      // the next S image (this tile's next ResBlock, or the next tile's first) and the residual
-      // rows are loaded two steps before the end of c2 (latency hidden, registers held briefly)
-      const int jpf = k > 2 ? k - 2 : 0;
+      // Step 0 also issues the next S image's rows (this tile's next ResBlock, or the next tile's
+      // first) and the residual rows, after its weight pieces; peeled out of the step loop so that
+      // no load is pending across the loop's back edge (hipcc then waited for them at the top).
+      const float* nsrc = !last_m ? p.src[m + 1] + cb0 : p.src[0] + (long long)nb * p.bstride;
+      const int nsr0 = !last_m ? r0 : nr0;
       f32x4 res[RB][2];
-      for (int j = 0; j < k; ++j) {
+      auto c2_weights = [&](int j) {
         if (j + 1 < k) issue_w(wtap(m, 1, j + 1), slot ^ 1);
         else if (has_next) issue_w(wtap(last_m ? 0 : m + 1, 0, 0), slot ^ 1);
-        int younger = 0;
-        if (j == jpf) {
-          younger = 2 * RB + (has_next ? 2 * NIT : 0);
-          if (has_next) {
-            if (!last_m) issue_fill(p.src[m + 1] + cb0, r0);
-            else issue_fill(p.src[0] + (long long)nb * p.bstride, nr0);
-          }
+      };
+      RP_T(u0);
+      c2_weights(0);
+      RP_T(u1);
+      if (has_next) issue_fill(nsrc, nsr0);
+      RP_T(u2);
 #pragma unroll
-          for (int i = 0; i < RB; ++i) {
-            const int q = min(r0 + (wr + WR * i) * 16 + l15, L - 1);
+      for (int i = 0; i < RB; ++i) {
+        const int q = min(r0 + (wr + WR * i) * 16 + l15, L - 1);
 #pragma unroll
-            for (int cb = 0; cb < 2; ++cb) {
-              const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
-              res[i][cb] = *reinterpret_cast<const f32x4*>(p.src[m] + cb0 + (long long)q * C + c0);
-            }
-          }
+        for (int cb = 0; cb < 2; ++cb) {
+          const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+          res[i][cb] = *reinterpret_cast<const f32x4*>(p.src[m] + cb0 + (long long)q * C + c0);
         }
+      }
+      RP_T(u3);
+      mfma_step(acc, slot, 8 - hk, nrb2);
+      RP_T(u4);
+      rp_wait(2 * RB + (has_next ? 2 * NIT : 0));
+      RP_T(u5);
+      rp_barrier();
+      RP_T(td);
+#ifdef RP_DIAG_STAMPS
+      dg[13] += u2 - u0; dg[14] += u3 - u2; dg[15] += (u4 - u3) * 1000000ull + (u5 - u4);
+#endif
+      slot ^= 1;
+      for (int j = 1; j < k; ++j) {
+        c2_weights(j);
         mfma_step(acc, slot, 8 + j - hk, nrb2);
-        rp_wait(younger);
+#ifndef RP_DIAG_NOBAR
+        rp_wait(0);
         rp_barrier();
+#endif
         slot ^= 1;
       }
+      RP_T(te);
       // ---- epilogue: state + c2 + b2 (rows past the clip end are dropped)
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
-        const f32x4 bias = *reinterpret_cast<const f32x4*>(p.b2[m] + c0);
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(bias_lds + (kMaxGroup + m) * C + c0);
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
           if (i >= nrb2) break;
@@ -303,17 +371,40 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
           }
         }
       }
+      RP_T(tf);
       if (has_next) {
-        commit_fill(last_m ? nr0 : r0);
+        commit_fill(nsr0);
         rp_barrier();
       }
+#ifdef RP_DIAG_STAMPS
+      {
+        RP_T(tg);
+        dg[0] += tb - ta; dg[1] += tc - tb; dg[2] += td - tc; dg[3] += te - td; dg[4] += tf - te; dg[5] += tg - tf;
+        dg[6] += 1; dg[7] += k; dg[8] += k;
+      }
+#endif
     }
     if (!more) break;
     tile = next_tile;
     b = nb;
     r0 = nr0;
   }
+#ifdef RP_DIAG_STAMPS
+  if (tid == 0)
+    for (int i = 0; i < 16; ++i) atomicAdd(&g_rp_diag[(C == 64 ? 16 : 0) + i], dg[i]);
+#endif
 }
+
+#ifdef RP_DIAG_STAMPS
+extern "C" int dcx_diag_rp(unsigned long long* out32, int reset) {
+  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_rp_diag), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned long long z[32] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_rp_diag), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** kname) {
   if (p.nmem < 1 || p.nmem > kMaxGroup || p.batch < 1 || p.L < 1 || (p.C != 32 && p.C != 64))
