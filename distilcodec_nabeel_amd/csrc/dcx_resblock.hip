@@ -51,7 +51,7 @@ __device__ __forceinline__ void rp_wait(int n) {
 #define RP_W(k) \
   case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
   switch (n) {
-    RP_W(8) RP_W(10) RP_W(14) RP_W(16) RP_W(18) RP_W(24) RP_W(26)
+    RP_W(1) RP_W(2) RP_W(3) RP_W(4) RP_W(5) RP_W(6) RP_W(7) RP_W(8) RP_W(9) RP_W(10) RP_W(11) RP_W(12)
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 #undef RP_W
@@ -59,8 +59,8 @@ __device__ __forceinline__ void rp_wait(int n) {
 
 #ifdef RP_DIAG_STAMPS
 // Diagnostic build only: shader-clock sums per phase of conv_res_pair (wave 0 of every workgroup):
-// [0] c1 steps, [1] T image, [2] c2 step 0 (with the prefetch issue), [3] c2 steps 1.., [4] epilogue,
-// [5] next S image, [6] member-tiles, [7] c1 steps counted, [8] c2 steps counted.
+// [0] c1 steps, [1] T image, [2] c2 steps, [3] epilogue, [4] next S image, [5] member-tiles,
+// [6] c1 steps counted, [7] c2 steps counted, [8] c1 step MFMA phases, [9] c1 step barrier waits.
 __device__ unsigned long long g_rp_diag[32];  // [C == 64][16]
 #define RP_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #else
@@ -79,12 +79,15 @@ struct RpGeom {
   static constexpr int NB2 = R / 16, RB2 = (NB2 + WR - 1) / WR;
   static constexpr int BLK = NCH * 1536;         // bytes per 16-row block of an image
   static constexpr int IMG = NS / 16 * BLK;      // S image bytes (T reuses its start)
-  static constexpr int WSLOT = C * C * 6;        // one tap of weights
+  static constexpr int TPS = C == 32 ? 2 : 1;    // taps per step (weight slot)
+  static constexpr int WTAP = C * C * 6;         // one tap of weights
+  static constexpr int WSLOT = TPS * WTAP;
   static constexpr int G8 = C / 8;               // 8-channel groups per row
   static constexpr int NIT = (NS * G8 + 511) / 512;
-  static constexpr int WP = WSLOT / 1024, WPW = (WP + 7) / 8;  // DMA pieces per tap, per wave
+  static constexpr int WP = WSLOT / 1024, WPW = (WP + 7) / 8;  // DMA pieces per slot, per wave
+  static constexpr int LDS = IMG + 2 * WSLOT + 2 * kMaxGroup * C * 4;
   static_assert(NB1 % WR == 0 && RB1 == RB2, "row blocks per wave");
-  static_assert(IMG + 2 * WSLOT + 2 * kMaxGroup * C * 4 <= 160 * 1024, "LDS");
+  static_assert(WSLOT % 1024 == 0 && LDS <= 160 * 1024, "LDS");
 };
 
 }  // namespace
@@ -92,9 +95,9 @@ struct RpGeom {
 template <int C, bool MEAN>
 __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
   using G = RpGeom<C>;
-  constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB1, BLK = G::BLK, IMG = G::IMG;
-  constexpr int WSLOT = G::WSLOT, G8 = G::G8, NIT = G::NIT, WP = G::WP, WPW = G::WPW, NS = G::NS;
-  __shared__ __attribute__((aligned(16))) char lds[IMG + 2 * WSLOT + 2 * kMaxGroup * C * 4];
+  constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB1, BLK = G::BLK, IMG = G::IMG, TPS = G::TPS;
+  constexpr int WTAP = G::WTAP, WSLOT = G::WSLOT, G8 = G::G8, NIT = G::NIT, WP = G::WP, WPW = G::WPW, NS = G::NS;
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS];
   float* const bias_lds = reinterpret_cast<float*>(lds + IMG + 2 * WSLOT);  // [conv][member][C]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -104,39 +107,34 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
   const int ntl = (L + R - 1) / R;
   const int total = ntl * p.batch;
 
-  // ---- weight ring: LDS-DMA of one tap slice (lane-linear 1 KiB pieces, no staging registers) ----
-  auto issue_w = [&](const unsigned short* w, int slot) {
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)w, 0, WSLOT, 0x00020000);
+  // ---- weight ring: LDS-DMA of a step's taps (lane-linear 1 KiB pieces, no staging registers);
+  // taps past the conv's last read zeros (outside the buffer descriptor) and are never used ----
+  auto issue_w = [&](int m, int conv, int step, int slot) {
+    const int k = p.taps[m], j0 = step * TPS;
+    const unsigned short* w = (conv ? p.w2[m] : p.w1[m]) + (long long)j0 * (WTAP / 2);
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc((void*)w, 0, min(TPS, k - j0) * WTAP, 0x00020000);
 #pragma unroll
-    for (int k = 0; k < WPW; ++k) {
-      const int piece = wave + 8 * k;
+    for (int i = 0; i < WPW; ++i) {
+      const int piece = wave + 8 * i;
       if (WP % 8 == 0 || piece < WP)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (rp_lds_t)(lds + IMG + slot * WSLOT + piece * 1024), 16,
                                                  piece * 1024 + lane * 16, 0, 0, 0);
     }
     asm volatile("" ::: "memory");  // later loads stay younger than the pieces (rp_wait counts them)
   };
-  auto wtap = [&](int m, int conv, int j) -> const unsigned short* {
-    return (conv ? p.w2[m] : p.w1[m]) + (long long)j * (WSLOT / 2);
-  };
 
   // ---- S image fill: state rows -> registers (issue) -> silu, planes, LDS (commit) ----
   f32x4 pf[NIT][2];
-  auto issue_fill = [&](const float* src, int r0) {
-#pragma unroll
-    for (int k = 0; k < NIT; ++k) {
-      const int it = min(tid + 512 * k, NS * G8 - 1);  // unconditional (rp_wait counts the loads)
-      const int s = ((it >> 3) / G8) * 8 + (it & 7), g8 = (it >> 3) % G8;
-      const int a = min(max(r0 - 8 - G::H1 + s, 0), L - 1);
-      const f32x4* q = reinterpret_cast<const f32x4*>(src + (long long)a * C + g8 * 8);
-      pf[k][0] = q[0];
-      pf[k][1] = q[1];
-    }
+  auto issue_fill_item = [&](const float* src, int r0, int k) {
+    const int it = min(tid + 512 * k, NS * G8 - 1);  // unconditional (rp_wait counts the loads)
+    const int s = ((it >> 3) / G8) * 8 + (it & 7), g8 = (it >> 3) % G8;
+    const int a = min(max(r0 - 8 - G::H1 + s, 0), L - 1);
+    const f32x4* q = reinterpret_cast<const f32x4*>(src + (long long)a * C + g8 * 8);
+    pf[k][0] = q[0];
+    pf[k][1] = q[1];
   };
   auto commit_fill = [&](int r0) {
-#ifdef RP_DIAG_NOVALU
-    return;
-#endif
 #pragma unroll
     for (int k = 0; k < NIT; ++k) {
       const int it = tid + 512 * k;
@@ -147,16 +145,10 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
       s16x8 hv, mv, lv;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-#ifdef RP_DIAG_RAW
-        const float v = ok ? pf[k][e >> 2][e & 3] : 0.f;
-        const unsigned u = __float_as_uint(v);
-        unsigned short h = u >> 16, m = u & 0xffff, l = h;
-#else
         const float sv = rp_silu(pf[k][e >> 2][e & 3]);
         const float v = ok ? sv : 0.f;
         unsigned short h, m, l;
         split3(v, h, m, l);
-#endif
         hv[e] = (short)h;
         mv[e] = (short)m;
         lv[e] = (short)l;
@@ -168,56 +160,66 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
     }
   };
 
-  // ---- one step: every chunk of one tap, rows of this wave, its 2 column blocks ----
+  // ---- one step: the step's taps, every chunk, rows of this wave, its 2 column blocks.  hook(i)
+  // runs after row block i of the first tap (global loads spread between the MFMAs) ----
   const int soX0 = (hf * 3 + t) * 256, soX1 = (hf * 3 + (t ? 0 : 1)) * 256, soX2 = (hf * 3 + (t ? 0 : 2)) * 256;
-  auto mfma_step = [&](f32x4 (&acc)[RB][2], int slot, int rowoff, int nrb) {
-    const char* wb = lds + IMG + slot * WSLOT;
-    s16x8 wf[NCH][2][2];
+  auto mfma_step = [&](f32x4 (&acc)[RB][2], int slot, int ntaps, int row0, int rstep, int nrb, auto hook) {
 #pragma unroll
-    for (int ch = 0; ch < NCH; ++ch)
+    for (int u = 0; u < TPS; ++u) {
+      if (u >= ntaps) break;
+      const char* wb = lds + IMG + slot * WSLOT + u * WTAP;
+      s16x8 wf[NCH][2][2];
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const char* w = wb + (ch * C + (2 * wc + cb) * 16 + l15) * 96 + hf * 48;
-        wf[ch][cb][0] = *reinterpret_cast<const s16x8*>(w + t * 16);        // {h', m'}
-        wf[ch][cb][1] = *reinterpret_cast<const s16x8*>(w + (t ? 32 : 0));  // {h', l'}
-      }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < RB; ++i) {
-      if (i >= nrb) break;
-      const int sr = (wr + WR * i) * 16 + l15 + rowoff;
-      const char* xr = lds + (sr >> 4) * BLK + (sr & 15) * 16;
-#pragma unroll
-      for (int ch = 0; ch < NCH; ++ch) {
-        const s16x8 x2 = *reinterpret_cast<const s16x8*>(xr + ch * 1536 + soX2);
-        const s16x8 x1 = *reinterpret_cast<const s16x8*>(xr + ch * 1536 + soX1);
-        const s16x8 x0 = *reinterpret_cast<const s16x8*>(xr + ch * 1536 + soX0);
+      for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
-          acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][1]),
-                                                               __builtin_bit_cast(bf16x8, x2), acc[i][cb], 0, 0, 0);
-          acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][0]),
-                                                               __builtin_bit_cast(bf16x8, x1), acc[i][cb], 0, 0, 0);
-          acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][0]),
-                                                               __builtin_bit_cast(bf16x8, x0), acc[i][cb], 0, 0, 0);
+          const char* w = wb + (ch * C + (2 * wc + cb) * 16 + l15) * 96 + hf * 48;
+          wf[ch][cb][0] = *reinterpret_cast<const s16x8*>(w + t * 16);        // {h', m'}
+          wf[ch][cb][1] = *reinterpret_cast<const s16x8*>(w + (t ? 32 : 0));  // {h', l'}
         }
+      const int rowoff = row0 + u * rstep;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        if (i < nrb) {
+          const int sr = (wr + WR * i) * 16 + l15 + rowoff;
+          const char* xr = lds + (sr >> 4) * BLK + (sr & 15) * 16;
+#pragma unroll
+          for (int ch = 0; ch < NCH; ++ch) {
+            const s16x8 x2 = *reinterpret_cast<const s16x8*>(xr + ch * 1536 + soX2);
+            const s16x8 x1 = *reinterpret_cast<const s16x8*>(xr + ch * 1536 + soX1);
+            const s16x8 x0 = *reinterpret_cast<const s16x8*>(xr + ch * 1536 + soX0);
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+              acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][1]),
+                                                                   __builtin_bit_cast(bf16x8, x2), acc[i][cb], 0, 0, 0);
+              acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][0]),
+                                                                   __builtin_bit_cast(bf16x8, x1), acc[i][cb], 0, 0, 0);
+              acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][0]),
+                                                                   __builtin_bit_cast(bf16x8, x0), acc[i][cb], 0, 0, 0);
+            }
+          }
+        }
+        if (u == 0) hook(i);
       }
+      __builtin_amdgcn_s_setprio(0);
     }
-    __builtin_amdgcn_s_setprio(0);
   };
+  auto no_hook = [](int) {};
 
   // rows of c2 this wave owns
   const int nrb2 = min(RB, (G::NB2 - wr + WR - 1) / WR);
   int tile = blockIdx.x;
   if (tile >= total) return;  // whole workgroup, before any barrier
   int b = tile / ntl, r0 = (tile - b * ntl) * R;
-  // prologue: first ResBlock's S image and first weight tap
+  // prologue: biases, first ResBlock's S image and first weight step
   if (tid < 2 * nmem * C) {
     const int conv = tid / (nmem * C), m = (tid / C) % nmem, c = tid % C;
     bias_lds[(conv * kMaxGroup + m) * C + c] = (conv ? p.b2[m] : p.b1[m])[c];
   }
-  issue_w(wtap(0, 0, 0), 0);
-  issue_fill(p.src[0] + (long long)b * p.bstride, r0);
+  issue_w(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) issue_fill_item(p.src[0] + (long long)b * p.bstride, r0, k);
   commit_fill(r0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   rp_barrier();
@@ -232,117 +234,113 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
     const int nb = more ? next_tile / ntl : 0, nr0 = more ? (next_tile - nb * ntl) * R : 0;
     for (int m = 0; m < nmem; ++m) {
       const int k = p.taps[m], hk = (k - 1) >> 1, d = p.dil[m];
+      const int nst = (k + TPS - 1) / TPS;  // steps per conv
       const long long cb0 = (long long)b * p.bstride;
+      const bool last_m = m + 1 == nmem;
+      const bool has_next = !last_m || more;
       f32x4 acc[RB][2];
       RP_T(ta);
       // ---- c1 over rows [r0 - 8, r0 + R + 8) from the S image
 #pragma unroll
       for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int j = 0; j < k; ++j) {
-        RP_T(s0);
-        issue_w(j + 1 < k ? wtap(m, 0, j + 1) : wtap(m, 1, 0), slot ^ 1);
+      for (int j = 0; j < nst; ++j) {
+        if (j + 1 < nst) issue_w(m, 0, j + 1, slot ^ 1);
+        else issue_w(m, 1, 0, slot ^ 1);
         RP_T(s1);
-        mfma_step(acc, slot, G::H1 + (j - hk) * d, RB);
+        mfma_step(acc, slot, min(TPS, k - j * TPS), G::H1 + (j * TPS - hk) * d, d, RB, no_hook);
         RP_T(s2);
-#ifndef RP_DIAG_NOBAR
         rp_wait(0);
-        RP_T(s3);
         rp_barrier();
-#endif
 #ifdef RP_DIAG_STAMPS
         {
-          RP_T(s4);
-          dg[9] += s1 - s0; dg[10] += s2 - s1; dg[11] += s3 - s2; dg[12] += s4 - s3;
+          RP_T(s3);
+          dg[8] += s2 - s1;
+          dg[9] += s3 - s2;
         }
 #endif
         slot ^= 1;
       }
       RP_T(tb);
       // ---- T image: silu(c1 + b1) planes over the S image (zero outside the clip)
-#ifndef RP_DIAG_NOVALU
-      {
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
-          const f32x4 bias = *reinterpret_cast<const f32x4*>(bias_lds + m * C + c0);
+      for (int cb = 0; cb < 2; ++cb) {
+        const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(bias_lds + m * C + c0);
 #pragma unroll
-          for (int i = 0; i < RB; ++i) {
-            const int ir = (wr + WR * i) * 16 + l15, a = r0 - 8 + ir;
-            const bool ok = a >= 0 && a < L;
-            s16x4 hv, mv, lv;
+        for (int i = 0; i < RB; ++i) {
+          const int ir = (wr + WR * i) * 16 + l15, a = r0 - 8 + ir;
+          const bool ok = a >= 0 && a < L;
+          s16x4 hv, mv, lv;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-#ifdef RP_DIAG_RAW
-              const float v = ok ? acc[i][cb][e] + bias[e] : 0.f;
-              const unsigned u = __float_as_uint(v);
-              unsigned short h = u >> 16, mm = u & 0xffff, l = h;
-#else
-              const float sv = rp_silu(acc[i][cb][e] + bias[e]);
-              const float v = ok ? sv : 0.f;
-              unsigned short h, mm, l;
-              split3(v, h, mm, l);
-#endif
-              hv[e] = (short)h;
-              mv[e] = (short)mm;
-              lv[e] = (short)l;
-            }
-            char* dst = lds + (ir >> 4) * BLK + (c0 >> 4) * 1536 + ((c0 >> 3) & 1) * 768 + (ir & 15) * 16 + (c0 & 7) * 2;
-            *reinterpret_cast<s16x4*>(dst) = hv;
-            *reinterpret_cast<s16x4*>(dst + 256) = mv;
-            *reinterpret_cast<s16x4*>(dst + 512) = lv;
+          for (int e = 0; e < 4; ++e) {
+            const float sv = rp_silu(acc[i][cb][e] + bias[e]);
+            const float v = ok ? sv : 0.f;
+            unsigned short h, mm, l;
+            split3(v, h, mm, l);
+            hv[e] = (short)h;
+            mv[e] = (short)mm;
+            lv[e] = (short)l;
           }
+          char* dst = lds + (ir >> 4) * BLK + (c0 >> 4) * 1536 + ((c0 >> 3) & 1) * 768 + (ir & 15) * 16 + (c0 & 7) * 2;
+          *reinterpret_cast<s16x4*>(dst) = hv;
+          *reinterpret_cast<s16x4*>(dst + 256) = mv;
+          *reinterpret_cast<s16x4*>(dst + 512) = lv;
         }
       }
-#endif
       rp_barrier();
       RP_T(tc);
-      // ---- c2 over rows [r0, r0 + R) from the T image; residual rows prefetched
+      // ---- c2 over rows [r0, r0 + R) from the T image.  Step 0 loads the residual rows, step 1 (or
+      // 0) the next S image's rows (this tile's next ResBlock, or the next tile's first), one row
+      // block's share between the MFMAs of each, after the step's weight pieces.  The two steps are
+      // peeled out of the loop: a load pending across the loop's back edge made hipcc wait for it.
 #pragma unroll
       for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const bool last_m = m + 1 == nmem;
-      const bool has_next = !last_m || more;
-      // Step 0 also issues the next S image's rows (this tile's next ResBlock, or the next tile's
-      // first) and the residual rows, after its weight pieces; peeled out of the step loop so that
-      // no load is pending across the loop's back edge (hipcc then waited for them at the top).
       const float* nsrc = !last_m ? p.src[m + 1] + cb0 : p.src[0] + (long long)nb * p.bstride;
       const int nsr0 = !last_m ? r0 : nr0;
+      const int jpf = nst > 1 ? 1 : 0;
       f32x4 res[RB][2];
-      auto c2_weights = [&](int j) {
-        if (j + 1 < k) issue_w(wtap(m, 1, j + 1), slot ^ 1);
-        else if (has_next) issue_w(wtap(last_m ? 0 : m + 1, 0, 0), slot ^ 1);
-      };
-      RP_T(u0);
-      c2_weights(0);
-      RP_T(u1);
-      if (has_next) issue_fill(nsrc, nsr0);
-      RP_T(u2);
-#pragma unroll
-      for (int i = 0; i < RB; ++i) {
+      auto res_hook = [&](int i) {
         const int q = min(r0 + (wr + WR * i) * 16 + l15, L - 1);
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
           const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
           res[i][cb] = *reinterpret_cast<const f32x4*>(p.src[m] + cb0 + (long long)q * C + c0);
         }
+      };
+      auto pf_hook = [&](int i) {
+        if (!has_next) return;
+#pragma unroll
+        for (int kk = NIT * i / RB; kk < NIT * (i + 1) / RB; ++kk) issue_fill_item(nsrc, nsr0, kk);
+      };
+      auto both_hook = [&](int i) {
+        res_hook(i);
+        pf_hook(i);
+      };
+      auto c2_issue_w = [&](int j) {
+        if (j + 1 < nst) issue_w(m, 1, j + 1, slot ^ 1);
+        else if (has_next) issue_w(last_m ? 0 : m + 1, 0, 0, slot ^ 1);
+      };
+      const int npf = has_next ? 2 * NIT : 0;
+      c2_issue_w(0);
+      if (jpf == 0) {
+        mfma_step(acc, slot, min(TPS, k), 8 - hk, 1, nrb2, both_hook);
+        rp_wait(2 * RB + npf);
+      } else {
+        mfma_step(acc, slot, TPS, 8 - hk, 1, nrb2, res_hook);
+        rp_wait(2 * RB);
+        rp_barrier();
+        slot ^= 1;
+        c2_issue_w(1);
+        mfma_step(acc, slot, min(TPS, k - TPS), 8 + TPS - hk, 1, nrb2, pf_hook);
+        rp_wait(npf);
       }
-      RP_T(u3);
-      mfma_step(acc, slot, 8 - hk, nrb2);
-      RP_T(u4);
-      rp_wait(2 * RB + (has_next ? 2 * NIT : 0));
-      RP_T(u5);
       rp_barrier();
-      RP_T(td);
-#ifdef RP_DIAG_STAMPS
-      dg[13] += u2 - u0; dg[14] += u3 - u2; dg[15] += (u4 - u3) * 1000000ull + (u5 - u4);
-#endif
       slot ^= 1;
-      for (int j = 1; j < k; ++j) {
-        c2_weights(j);
-        mfma_step(acc, slot, 8 + j - hk, nrb2);
-#ifndef RP_DIAG_NOBAR
+      for (int j = jpf + 1; j < nst; ++j) {
+        c2_issue_w(j);
+        mfma_step(acc, slot, min(TPS, k - j * TPS), 8 + j * TPS - hk, 1, nrb2, no_hook);
         rp_wait(0);
         rp_barrier();
-#endif
         slot ^= 1;
       }
       RP_T(te);
@@ -379,8 +377,8 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
 #ifdef RP_DIAG_STAMPS
       {
         RP_T(tg);
-        dg[0] += tb - ta; dg[1] += tc - tb; dg[2] += td - tc; dg[3] += te - td; dg[4] += tf - te; dg[5] += tg - tf;
-        dg[6] += 1; dg[7] += k; dg[8] += k;
+        dg[0] += tb - ta; dg[1] += tc - tb; dg[2] += te - tc; dg[3] += tf - te; dg[4] += tg - tf;
+        dg[5] += 1; dg[6] += nst; dg[7] += nst;
       }
 #endif
     }

@@ -22,19 +22,16 @@ for _ in range(2):
     eng.generate(z)
 torch.cuda.synchronize()
 L.dcx_diag_rp(buf, 1)
-names = ["c1 steps", "T image", "c2 step 0", "c2 steps 1..", "epilogue", "next S image"]
+names = ["c1 steps", "T image", "c2 steps", "epilogue", "next S image"]
 for ci, C in enumerate((32, 64)):
     v = list(buf)[ci * 16:(ci + 1) * 16]
-    n, s1, s2 = v[6], v[7], v[8]
-    tot = sum(v[:6])
+    n, s1, s2 = v[5], v[6], v[7]
+    tot = sum(v[:5])
     print(f"C = {C}: {n} member-tiles (wave 0 of each workgroup), {tot / n:.0f} cycles per member-tile")
     for i, nm in enumerate(names):
         extra = ""
         if i == 0:
-            extra = f"  {v[0] / s1:.0f} per step"
-        if i == 3:
-            extra = f"  {v[3] / (s2 - n):.0f} per step"
+            extra = f"  {v[0] / s1:.0f} per step (MFMA phase {v[8] / s1:.0f}, wait + barrier {v[9] / s1:.0f})"
+        if i == 2:
+            extra = f"  {v[2] / s2:.0f} per step"
         print(f"   {nm:14s} {v[i] / n:8.0f} cycles ({v[i] / tot:5.1%}){extra}")
-    print(f"   c1 step: DMA issue {v[9] / s1:.0f}, MFMA phase {v[10] / s1:.0f}, vmcnt wait {v[11] / s1:.0f}, barrier {v[12] / s1:.0f}")
-    print(f"   c2 step 0: DMA issue + prefetch issue {v[13] / n:.0f}, residual issue {v[14] / n:.0f}, "
-          f"MFMA phase {(v[15] // 1000000) / n:.0f}, vmcnt wait {(v[15] % 1000000) / n:.0f}")
