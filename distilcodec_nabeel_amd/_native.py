@@ -81,6 +81,10 @@ SIGNATURES = {
     "dcx_generate": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _SZ, _P]),
     "dcx_encode_decode": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _SZ, _P]),
     "dcx_transpose": (ctypes.c_int, [_P, _P, _I32, _I64, _I64, _P]),
+    "dcx_mp3_info": (ctypes.c_int, [_P, _SZ, ctypes.POINTER(_I64), ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
+    "dcx_mp3_decode": (ctypes.c_int, [_P, _SZ, _P, _I64]),
+    "dcx_mp3_last_error": (ctypes.c_char_p, []),
+    "dcx_mp3_stats": (ctypes.c_int, [ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
     "dcx_resample_poly": (ctypes.c_int, [_P, _I32, _I64, _I64, _P, _I32, _I32, _I32, _I64, _P, _I64, _I64, _P]),
     "dcx_set_gemm_mode": (ctypes.c_int, [_P, _I32]),
     "dcx_get_gemm_mode": (_I32, [_P]),

@@ -1,0 +1,662 @@
+// MPEG-1 Layer III decoder (host code): the file front end of the reference's demo path.
+//
+// The reference reads every input with librosa.load (distilcodec/models/meldataset.py:18-20,
+// distil_codec.py:667), which decodes MP3 through libsndfile/mpg123 or audioread/ffmpeg; C1's input
+// is the MP3 test.mp3 (README.md:116).  None of those decoders exists in this image, so this is a
+// from-scratch restatement of ISO/IEC 11172-3 Layer III: frame headers, side information and the
+// bit reservoir, scalefactors (scfsi), Huffman decoding (big_values regions, linbits, count1),
+// requantisation, short-block reordering, mid/side stereo, alias reduction, IMDCT with the four
+// window shapes and overlap-add, frequency inversion and the 32-band polyphase synthesis
+// filterbank.  Gapless trimming follows the Xing/LAME header like mpg123 and ffmpeg: the encoder
+// delay plus the 529-sample decoder delay is skipped and the encoder padding dropped.
+//
+// Tables: the Huffman code books of Annex B (checked prefix-free and complete: Kraft sum 1) and the
+// synthesis window D[i] of Table 3-B.3 (integer multiples of 2^-16; its prototype lowpass is -3.01 dB
+// at pi/64 with > 104 dB stop-band attenuation, tests/test_mp3.py).
+// Not supported (the call fails with DCX_ERR_INVALID_ARG): MPEG-2 / 2.5 (LSF) streams, free-format
+// bitrates and intensity stereo (which LAME does not emit).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/distilcodec_amd.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// Huffman code books (ISO/IEC 11172-3 Annex B, Table B.7): codes and lengths, x-major order
+// ---------------------------------------------------------------------------------------------
+const uint16_t kH1c[] = {1,1,1,0};
+const uint8_t kH1l[] = {1,3,2,3};
+const uint16_t kH2c[] = {1,2,1,3,1,1,3,2,0};
+const uint8_t kH2l[] = {1,3,6,3,3,5,5,5,6};
+const uint16_t kH3c[] = {3,2,1,1,1,1,3,2,0};
+const uint8_t kH3l[] = {2,2,6,3,2,5,5,5,6};
+const uint16_t kH5c[] = {1,2,6,5,3,1,4,4,7,5,7,1,6,1,1,0};
+const uint8_t kH5l[] = {1,3,6,7,3,3,6,7,6,6,7,8,7,6,7,8};
+const uint16_t kH6c[] = {7,3,5,1,6,2,3,2,5,4,4,1,3,3,2,0};
+const uint8_t kH6l[] = {3,3,5,7,3,2,4,5,4,4,5,6,6,5,6,7};
+const uint16_t kH7c[] = {1,2,10,19,16,10,3,3,7,10,5,3,11,4,13,17,8,4,12,11,18,15,11,2,7,6,9,14,3,1,6,4,5,3,2,0};
+const uint8_t kH7l[] = {1,3,6,8,8,9,3,4,6,7,7,8,6,5,7,8,8,9,7,7,8,9,9,9,7,7,8,9,9,10,8,8,9,10,10,10};
+const uint16_t kH8c[] = {3,4,6,18,12,5,5,1,2,16,9,3,7,3,5,14,7,3,19,17,15,13,10,4,13,5,8,11,5,1,12,4,4,1,1,0};
+const uint8_t kH8l[] = {2,3,6,8,8,9,3,2,4,8,8,8,6,4,6,8,8,9,8,8,8,9,9,10,8,7,8,9,10,10,9,8,9,9,11,11};
+const uint16_t kH9c[] = {7,5,9,14,15,7,6,4,5,5,6,7,7,6,8,8,8,5,15,6,9,10,5,1,11,7,9,6,4,1,14,4,6,2,6,0};
+const uint8_t kH9l[] = {3,3,5,6,8,9,3,3,4,5,6,8,4,4,5,6,7,8,6,5,6,7,7,8,7,6,7,7,8,9,8,7,8,8,9,9};
+const uint16_t kH10c[] = {1,2,10,23,35,30,12,17,3,3,8,12,18,21,12,7,11,9,15,21,32,40,19,6,14,13,22,34,46,23,18,7,20,19,33,47,27,22,9,3,31,22,41,26,21,20,5,3,14,13,10,11,16,6,5,1,9,8,7,8,4,4,2,0};
+const uint8_t kH10l[] = {1,3,6,8,9,9,9,10,3,4,6,7,8,9,8,8,6,6,7,8,9,10,9,9,7,7,8,9,10,10,9,10,8,8,9,10,10,10,10,10,9,9,10,10,11,11,10,11,8,8,9,10,10,10,11,11,9,8,9,10,10,11,11,11};
+const uint16_t kH11c[] = {3,4,10,24,34,33,21,15,5,3,4,10,32,17,11,10,11,7,13,18,30,31,20,5,25,11,19,59,27,18,12,5,35,33,31,58,30,16,7,5,28,26,32,19,17,15,8,14,14,12,9,13,14,9,4,1,11,4,6,6,6,3,2,0};
+const uint8_t kH11l[] = {2,3,5,7,8,9,8,9,3,3,4,6,8,8,7,8,5,5,6,7,8,9,8,8,7,6,7,9,8,10,8,9,8,8,8,9,9,10,9,10,8,8,9,10,10,11,10,11,8,7,7,8,9,10,10,10,8,7,8,9,10,10,10,10};
+const uint16_t kH12c[] = {9,6,16,33,41,39,38,26,7,5,6,9,23,16,26,11,17,7,11,14,21,30,10,7,17,10,15,12,18,28,14,5,32,13,22,19,18,16,9,5,40,17,31,29,17,13,4,2,27,12,11,15,10,7,4,1,27,12,8,12,6,3,1,0};
+const uint8_t kH12l[] = {4,3,5,7,8,9,9,9,3,3,4,5,7,7,8,8,5,4,5,6,7,8,7,8,6,5,6,6,7,8,8,8,7,6,7,7,8,8,8,9,8,7,8,8,8,9,8,9,8,7,7,8,8,9,9,10,9,8,8,9,9,9,9,10};
+const uint16_t kH13c[] = {1,5,14,21,34,51,46,71,42,52,68,52,67,44,43,19,3,4,12,19,31,26,44,33,31,24,32,24,31,35,22,14,15,13,23,36,59,49,77,65,29,40,30,40,27,33,42,16,22,20,37,61,56,79,73,64,43,76,56,37,26,31,25,14,35,16,60,57,97,75,114,91,54,73,55,41,48,53,23,24,58,27,50,96,76,70,93,84,77,58,79,29,74,49,41,17,47,45,78,74,115,94,90,79,69,83,71,50,59,38,36,15,72,34,56,95,92,85,91,90,86,73,77,65,51,44,43,42,43,20,30,44,55,78,72,87,78,61,46,54,37,30,20,16,53,25,41,37,44,59,54,81,66,76,57,54,37,18,39,11,35,33,31,57,42,82,72,80,47,58,55,21,22,26,38,22,53,25,23,38,70,60,51,36,55,26,34,23,27,14,9,7,34,32,28,39,49,75,30,52,48,40,52,28,18,17,9,5,45,21,34,64,56,50,49,45,31,19,12,15,10,7,6,3,48,23,20,39,36,35,53,21,16,23,13,10,6,1,4,2,16,15,17,27,25,20,29,11,17,12,16,8,1,1,0,1};
+const uint8_t kH13l[] = {1,4,6,7,8,9,9,10,9,10,11,11,12,12,13,13,3,4,6,7,8,8,9,9,9,9,10,10,11,12,12,12,6,6,7,8,9,9,10,10,9,10,10,11,11,12,13,13,7,7,8,9,9,10,10,10,10,11,11,11,11,12,13,13,8,7,9,9,10,10,11,11,10,11,11,12,12,13,13,14,9,8,9,10,10,10,11,11,11,11,12,11,13,13,14,14,9,9,10,10,11,11,11,11,11,12,12,12,13,13,14,14,10,9,10,11,11,11,12,12,12,12,13,13,13,14,16,16,9,8,9,10,10,11,11,12,12,12,12,13,13,14,15,15,10,9,10,10,11,11,11,13,12,13,13,14,14,14,16,15,10,10,10,11,11,12,12,13,12,13,14,13,14,15,16,17,11,10,10,11,12,12,12,12,13,13,13,14,15,15,15,16,11,11,11,12,12,13,12,13,14,14,15,15,15,16,16,16,12,11,12,13,13,13,14,14,14,14,14,15,16,15,16,16,13,12,12,13,13,13,15,14,14,17,15,15,15,17,16,16,12,12,13,14,14,14,15,14,15,15,16,16,19,18,19,16};
+const uint16_t kH15c[] = {7,12,18,53,47,76,124,108,89,123,108,119,107,81,122,63,13,5,16,27,46,36,61,51,42,70,52,83,65,41,59,36,19,17,15,24,41,34,59,48,40,64,50,78,62,80,56,33,29,28,25,43,39,63,55,93,76,59,93,72,54,75,50,29,52,22,42,40,67,57,95,79,72,57,89,69,49,66,46,27,77,37,35,66,58,52,91,74,62,48,79,63,90,62,40,38,125,32,60,56,50,92,78,65,55,87,71,51,73,51,70,30,109,53,49,94,88,75,66,122,91,73,56,42,64,44,21,25,90,43,41,77,73,63,56,92,77,66,47,67,48,53,36,20,71,34,67,60,58,49,88,76,67,106,71,54,38,39,23,15,109,53,51,47,90,82,58,57,48,72,57,41,23,27,62,9,86,42,40,37,70,64,52,43,70,55,42,25,29,18,11,11,118,68,30,55,50,46,74,65,49,39,24,16,22,13,14,7,91,44,39,38,34,63,52,45,31,52,28,19,14,8,9,3,123,60,58,53,47,43,32,22,37,24,17,12,15,10,2,1,71,37,34,30,28,20,17,26,21,16,10,6,8,6,2,0};
+const uint8_t kH15l[] = {3,4,5,7,7,8,9,9,9,10,10,11,11,11,12,13,4,3,5,6,7,7,8,8,8,9,9,10,10,10,11,11,5,5,5,6,7,7,8,8,8,9,9,10,10,11,11,11,6,6,6,7,7,8,8,9,9,9,10,10,10,11,11,11,7,6,7,7,8,8,9,9,9,9,10,10,10,11,11,11,8,7,7,8,8,8,9,9,9,9,10,10,11,11,11,12,9,7,8,8,8,9,9,9,9,10,10,10,11,11,12,12,9,8,8,9,9,9,9,10,10,10,10,10,11,11,11,12,9,8,8,9,9,9,9,10,10,10,10,11,11,12,12,12,9,8,9,9,9,9,10,10,10,11,11,11,11,12,12,12,10,9,9,9,10,10,10,10,10,11,11,11,11,12,13,12,10,9,9,9,10,10,10,10,11,11,11,11,12,12,12,13,11,10,9,10,10,10,11,11,11,11,11,11,12,12,13,13,11,10,10,10,10,11,11,11,11,12,12,12,12,12,13,13,12,11,11,11,11,11,11,11,12,12,12,12,13,13,12,13,12,11,11,11,11,11,11,12,12,12,12,12,13,13,13,13};
+const uint16_t kH16c[] = {1,5,14,44,74,63,110,93,172,149,138,242,225,195,376,17,3,4,12,20,35,62,53,47,83,75,68,119,201,107,207,9,15,13,23,38,67,58,103,90,161,72,127,117,110,209,206,16,45,21,39,69,64,114,99,87,158,140,252,212,199,387,365,26,75,36,68,65,115,101,179,164,155,264,246,226,395,382,362,9,66,30,59,56,102,185,173,265,142,253,232,400,388,378,445,16,111,54,52,100,184,178,160,133,257,244,228,217,385,366,715,10,98,48,91,88,165,157,148,261,248,407,397,372,380,889,884,8,85,84,81,159,156,143,260,249,427,401,392,383,727,713,708,7,154,76,73,141,131,256,245,426,406,394,384,735,359,710,352,11,139,129,67,125,247,233,229,219,393,743,737,720,885,882,439,4,243,120,118,115,227,223,396,746,742,736,721,712,706,223,436,6,202,224,222,218,216,389,386,381,364,888,443,707,440,437,1728,4,747,211,210,208,370,379,734,723,714,1735,883,877,876,3459,865,2,377,369,102,187,726,722,358,711,709,866,1734,871,3458,870,434,0,12,10,7,11,10,17,11,9,13,12,10,7,5,3,1,3};
+const uint8_t kH16l[] = {1,4,6,8,9,9,10,10,11,11,11,12,12,12,13,9,3,4,6,7,8,9,9,9,10,10,10,11,12,11,12,8,6,6,7,8,9,9,10,10,11,10,11,11,11,12,12,9,8,7,8,9,9,10,10,10,11,11,12,12,12,13,13,10,9,8,9,9,10,10,11,11,11,12,12,12,13,13,13,9,9,8,9,9,10,11,11,12,11,12,12,13,13,13,14,10,10,9,9,10,11,11,11,11,12,12,12,12,13,13,14,10,10,9,10,10,11,11,11,12,12,13,13,13,13,15,15,10,10,10,10,11,11,11,12,12,13,13,13,13,14,14,14,10,11,10,10,11,11,12,12,13,13,13,13,14,13,14,13,11,11,11,10,11,12,12,12,12,13,14,14,14,15,15,14,10,12,11,11,11,12,12,13,14,14,14,14,14,14,13,14,11,12,12,12,12,12,13,13,13,13,15,14,14,14,14,16,11,14,12,12,12,13,13,14,14,14,16,15,15,15,17,15,11,13,13,11,12,14,14,13,14,14,15,16,15,17,15,14,11,9,8,8,9,9,10,10,10,11,11,11,11,11,11,11,8};
+const uint16_t kH24c[] = {15,13,46,80,146,262,248,434,426,669,653,649,621,517,1032,88,14,12,21,38,71,130,122,216,209,198,327,345,319,297,279,42,47,22,41,74,68,128,120,221,207,194,182,340,315,295,541,18,81,39,75,70,134,125,116,220,204,190,178,325,311,293,271,16,147,72,69,135,127,118,112,210,200,188,352,323,306,285,540,14,263,66,129,126,119,114,214,202,192,180,341,317,301,281,262,12,249,123,121,117,113,215,206,195,185,347,330,308,291,272,520,10,435,115,111,109,211,203,196,187,353,332,313,298,283,531,381,17,427,212,208,205,201,193,186,177,169,320,303,286,268,514,377,16,335,199,197,191,189,181,174,333,321,305,289,275,521,379,371,11,668,184,183,179,175,344,331,314,304,290,277,530,383,373,366,10,652,346,171,168,164,318,309,299,287,276,263,513,375,368,362,6,648,322,316,312,307,302,292,284,269,261,512,376,370,364,359,4,620,300,296,294,288,282,273,266,515,380,374,369,365,361,357,2,1033,280,278,274,267,264,259,382,378,372,367,363,360,358,356,0,43,20,19,17,15,13,11,9,7,6,4,7,5,3,1,3};
+const uint8_t kH24l[] = {4,4,6,7,8,9,9,10,10,11,11,11,11,11,12,9,4,4,5,6,7,8,8,9,9,9,10,10,10,10,10,8,6,5,6,7,7,8,8,9,9,9,9,10,10,10,11,7,7,6,7,7,8,8,8,9,9,9,9,10,10,10,10,7,8,7,7,8,8,8,8,9,9,9,10,10,10,10,11,7,9,7,8,8,8,8,9,9,9,9,10,10,10,10,10,7,9,8,8,8,8,9,9,9,9,10,10,10,10,10,11,7,10,8,8,8,9,9,9,9,10,10,10,10,10,11,11,8,10,9,9,9,9,9,9,9,9,10,10,10,10,11,11,8,10,9,9,9,9,9,9,10,10,10,10,10,11,11,11,8,11,9,9,9,9,10,10,10,10,10,10,11,11,11,11,8,11,10,9,9,9,10,10,10,10,10,10,11,11,11,11,8,11,10,10,10,10,10,10,10,10,10,11,11,11,11,11,8,11,10,10,10,10,10,10,10,11,11,11,11,11,11,11,8,12,10,10,10,10,10,10,11,11,11,11,11,11,11,11,8,8,7,7,7,7,7,7,7,7,7,7,8,8,8,8,4};
+
+struct Book {
+  const uint16_t* code;
+  const uint8_t* len;
+  int dim;
+};
+const Book kBooks[16] = {{nullptr, nullptr, 0}, {kH1c, kH1l, 2},   {kH2c, kH2l, 3},   {kH3c, kH3l, 3},
+                         {nullptr, nullptr, 0}, {kH5c, kH5l, 4},   {kH6c, kH6l, 4},   {kH7c, kH7l, 6},
+                         {kH8c, kH8l, 6},       {kH9c, kH9l, 6},   {kH10c, kH10l, 8}, {kH11c, kH11l, 8},
+                         {kH12c, kH12l, 8},     {kH13c, kH13l, 16}, {nullptr, nullptr, 0}, {kH15c, kH15l, 16}};
+const int kLinbits[32] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                          1, 2, 3, 4, 6, 8, 10, 13, 4, 5, 6, 7, 8, 9, 11, 13};
+// count1 table A (quadruples v w x y, index 8v + 4w + 2x + y)
+const uint8_t kQAc[16] = {1, 5, 4, 5, 6, 5, 4, 4, 7, 3, 6, 0, 7, 2, 3, 1};
+const uint8_t kQAl[16] = {1, 4, 4, 5, 4, 6, 5, 6, 4, 5, 5, 6, 5, 6, 6, 6};
+
+// Decoding tree per code book: node = {child0, child1}; a leaf stores ~value.
+struct Tree {
+  std::vector<int32_t> n;  // 2 entries per node
+  void build(const uint16_t* code, const uint8_t* len, int count) {
+    n.assign(2, 0);
+    for (int v = 0; v < count; ++v) {
+      int node = 0;
+      for (int b = len[v] - 1; b >= 0; --b) {
+        const int bit = (code[v] >> b) & 1;
+        if (b == 0) {
+          n[2 * node + bit] = ~v;
+        } else {
+          if (n[2 * node + bit] == 0) {
+            n[2 * node + bit] = (int32_t)(n.size() / 2);
+            n.push_back(0);
+            n.push_back(0);
+          }
+          node = n[2 * node + bit];
+        }
+      }
+    }
+  }
+};
+
+struct Trees {
+  Tree big[16], quad_a;
+  Trees() {
+    for (int i = 0; i < 16; ++i)
+      if (kBooks[i].code) big[i].build(kBooks[i].code, kBooks[i].len, kBooks[i].dim * kBooks[i].dim);
+    std::vector<uint16_t> qc(kQAc, kQAc + 16);
+    quad_a.build(qc.data(), kQAl, 16);
+  }
+};
+const Trees& trees() {
+  static const Trees t;
+  return t;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Synthesis window D[0..256] (Table 3-B.3) in units of 2^-16; D[512 - i] = -D[i] for i % 64 != 0,
+// D[i] for i = 64, 128, 192
+// ---------------------------------------------------------------------------------------------
+const int32_t kDwin[257] = {
+    0, -1, -1, -1, -1, -1, -1, -2, -2, -2, -2, -3, -3, -4, -4, -5,
+    -5, -6, -7, -7, -8, -9, -10, -11, -13, -14, -16, -17, -19, -21, -24, -26,
+    -29, -31, -35, -38, -41, -45, -49, -53, -58, -63, -68, -73, -79, -85, -91, -97,
+    -104, -111, -117, -125, -132, -139, -147, -154, -161, -169, -176, -183, -190, -196, -202, -208,
+    213, 218, 222, 225, 227, 228, 228, 227, 224, 221, 215, 208, 200, 189, 177, 163,
+    146, 127, 106, 83, 57, 29, -2, -36, -72, -111, -153, -197, -244, -294, -347, -401,
+    -459, -519, -581, -645, -711, -779, -848, -919, -991, -1064, -1137, -1210, -1283, -1356, -1428, -1498,
+    -1567, -1634, -1698, -1759, -1817, -1870, -1919, -1962, -2001, -2032, -2057, -2075, -2085, -2087, -2080, -2063,
+    2037, 2000, 1952, 1893, 1822, 1739, 1644, 1535, 1414, 1280, 1131, 970, 794, 605, 402, 185,
+    -45, -288, -545, -814, -1095, -1388, -1692, -2006, -2330, -2663, -3004, -3351, -3705, -4063, -4425, -4788,
+    -5153, -5517, -5879, -6237, -6589, -6935, -7271, -7597, -7910, -8209, -8491, -8755, -8998, -9219, -9416, -9585,
+    -9727, -9838, -9916, -9959, -9966, -9935, -9863, -9750, -9592, -9389, -9139, -8840, -8492, -8092, -7640, -7134,
+    6574, 5959, 5288, 4561, 3776, 2935, 2037, 1082, 70, -998, -2122, -3300, -4533, -5818, -7154, -8540,
+    -9975, -11455, -12980, -14548, -16155, -17799, -19478, -21189, -22929, -24694, -26482, -28289, -30112, -31947, -33791, -35640,
+    -37489, -39336, -41176, -43006, -44821, -46617, -48390, -50137, -51853, -53534, -55178, -56778, -58333, -59838, -61289, -62684,
+    -64019, -65290, -66494, -67629, -68692, -69679, -70590, -71420, -72169, -72835, -73415, -73908, -74313, -74630, -74856, -74992,
+    75038,
+};
+
+// scalefactor band boundaries (44.1, 48, 32 kHz): long [23], short [14]
+const int kSfbL[3][23] = {{0, 4, 8, 12, 16, 20, 24, 30, 36, 44, 52, 62, 74, 90, 110, 134, 162, 196, 238, 288, 342, 418, 576},
+                          {0, 4, 8, 12, 16, 20, 24, 30, 36, 42, 50, 60, 72, 88, 106, 128, 156, 190, 230, 276, 330, 384, 576},
+                          {0, 4, 8, 12, 16, 20, 24, 30, 36, 44, 54, 66, 82, 102, 126, 156, 194, 240, 296, 364, 448, 550, 576}};
+const int kSfbS[3][14] = {{0, 4, 8, 12, 16, 22, 30, 40, 52, 66, 84, 106, 136, 192},
+                          {0, 4, 8, 12, 16, 22, 28, 38, 50, 64, 80, 100, 126, 192},
+                          {0, 4, 8, 12, 16, 22, 30, 42, 58, 78, 104, 138, 180, 192}};
+const int kSlen[16][2] = {{0, 0}, {0, 1}, {0, 2}, {0, 3}, {3, 0}, {1, 1}, {1, 2}, {1, 3},
+                          {2, 1}, {2, 2}, {2, 3}, {3, 1}, {3, 2}, {3, 3}, {4, 2}, {4, 3}};
+const int kPretab[22] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 3, 2, 0};
+const int kBitrate[15] = {0, 32, 40, 48, 56, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320};
+const int kRate[3] = {44100, 48000, 32000};
+const int kDecoderDelay = 529;
+
+struct Header {
+  int protect, bitrate, rate_idx, padding, mode, mode_ext, channels, bytes;
+};
+
+bool parse_header(const uint8_t* p, Header& h) {
+  const uint32_t v = (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+  if ((v >> 21) != 0x7FF) return false;
+  if (((v >> 19) & 3) != 3 || ((v >> 17) & 3) != 1) return false;  // MPEG-1, Layer III
+  const int bi = (v >> 12) & 15, ri = (v >> 10) & 3;
+  if (bi == 0 || bi == 15 || ri == 3) return false;
+  h.protect = !((v >> 16) & 1);
+  h.bitrate = kBitrate[bi];
+  h.rate_idx = ri;
+  h.padding = (v >> 9) & 1;
+  h.mode = (v >> 6) & 3;
+  h.mode_ext = (v >> 4) & 3;
+  h.channels = h.mode == 3 ? 1 : 2;
+  h.bytes = 144000 * h.bitrate / kRate[ri] + h.padding;
+  return true;
+}
+
+struct Bits {
+  const uint8_t* p;
+  size_t n, pos;  // bits
+  uint32_t get(int k) {
+    uint32_t v = 0;
+    for (int i = 0; i < k; ++i) {
+      const size_t q = pos++;
+      v = (v << 1) | (q < n ? (p[q >> 3] >> (7 - (q & 7))) & 1 : 0);
+    }
+    return v;
+  }
+  int bit() { return (int)get(1); }
+};
+
+int tree_decode(const Tree& t, Bits& b) {
+  int node = 0;
+  for (int depth = 0; depth < 24; ++depth) {
+    const int32_t c = t.n[2 * node + b.bit()];
+    if (c < 0) return ~c;
+    if (c == 0) return -1;  // not a code word
+    node = c;
+  }
+  return -1;
+}
+
+struct Granule {
+  int part23, big_values, global_gain, sfc, wsf, block_type, mixed, table[3], sbg[3], r0, r1;
+  int preflag, sfs, c1table;
+};
+
+struct SideInfo {
+  int main_data_begin, scfsi[2][4];
+  Granule g[2][2];
+};
+
+void parse_side(Bits& b, int nch, SideInfo& s) {
+  s.main_data_begin = (int)b.get(9);
+  b.get(nch == 1 ? 5 : 3);
+  for (int ch = 0; ch < nch; ++ch)
+    for (int i = 0; i < 4; ++i) s.scfsi[ch][i] = b.bit();
+  for (int gr = 0; gr < 2; ++gr)
+    for (int ch = 0; ch < nch; ++ch) {
+      Granule& g = s.g[gr][ch];
+      g.part23 = (int)b.get(12);
+      g.big_values = (int)b.get(9);
+      g.global_gain = (int)b.get(8);
+      g.sfc = (int)b.get(4);
+      g.wsf = b.bit();
+      if (g.wsf) {
+        g.block_type = (int)b.get(2);
+        g.mixed = b.bit();
+        g.table[0] = (int)b.get(5);
+        g.table[1] = (int)b.get(5);
+        g.table[2] = 0;
+        for (int w = 0; w < 3; ++w) g.sbg[w] = (int)b.get(3);
+        g.r0 = g.block_type == 2 && !g.mixed ? 8 : 7;
+        g.r1 = 20 - g.r0;
+      } else {
+        g.block_type = g.mixed = 0;
+        for (int i = 0; i < 3; ++i) g.table[i] = (int)b.get(5);
+        g.sbg[0] = g.sbg[1] = g.sbg[2] = 0;
+        g.r0 = (int)b.get(4);
+        g.r1 = (int)b.get(3);
+      }
+      g.preflag = b.bit();
+      g.sfs = b.bit();
+      g.c1table = b.bit();
+    }
+}
+
+class Decoder {
+ public:
+  Decoder() {
+    std::memset(overlap_, 0, sizeof overlap_);
+    std::memset(v_, 0, sizeof v_);
+    for (int i = 0; i < 64; ++i)
+      for (int k = 0; k < 32; ++k) n_[i][k] = std::cos((16 + i) * (2 * k + 1) * M_PI / 64.0);
+    for (int i = 0; i < 257; ++i) dwin_[i] = kDwin[i] / 65536.0;
+    for (int i = 1; i < 256; ++i) dwin_[512 - i] = (i % 64 == 0 ? 1.0 : -1.0) * dwin_[i];
+    for (int i = 0; i < 36; ++i)
+      for (int k = 0; k < 18; ++k) cos36_[i][k] = std::cos(M_PI / 72.0 * (2 * i + 1 + 18) * (2 * k + 1));
+    for (int i = 0; i < 12; ++i)
+      for (int k = 0; k < 6; ++k) cos12_[i][k] = std::cos(M_PI / 24.0 * (2 * i + 1 + 6) * (2 * k + 1));
+    for (int i = 0; i < 36; ++i) {
+      const double s36 = std::sin(M_PI / 36.0 * (i + 0.5));
+      win_[0][i] = s36;
+      win_[1][i] = i < 18 ? s36 : i < 24 ? 1.0 : i < 30 ? std::sin(M_PI / 12.0 * (i - 18 + 0.5)) : 0.0;
+      win_[3][i] = i < 6 ? 0.0 : i < 12 ? std::sin(M_PI / 12.0 * (i - 6 + 0.5)) : i < 18 ? 1.0 : s36;
+      win_[2][i] = i < 12 ? std::sin(M_PI / 12.0 * (i + 0.5)) : 0.0;
+    }
+    static const double c[8] = {-0.6, -0.535, -0.33, -0.185, -0.095, -0.041, -0.0142, -0.0037};
+    for (int i = 0; i < 8; ++i) {
+      cs_[i] = 1.0 / std::sqrt(1.0 + c[i] * c[i]);
+      ca_[i] = c[i] / std::sqrt(1.0 + c[i] * c[i]);
+    }
+  }
+
+  // Decodes one frame (header already parsed) to 1152 samples per channel (out[ch][1152]).
+  // Returns false when the frame is not decodable (reservoir underflow, bad data, unsupported).
+  bool frame(const uint8_t* f, const Header& h, float* out[2], std::string& err) {
+    const int side_bytes = h.channels == 1 ? 17 : 32;
+    const int off = 4 + (h.protect ? 2 : 0);
+    if (h.bytes < off + side_bytes) {
+      err = "frame shorter than its side information";
+      return false;
+    }
+    Bits sb{f + off, (size_t)side_bytes * 8, 0};
+    SideInfo si;
+    parse_side(sb, h.channels, si);
+    if (h.mode == 1 && (h.mode_ext & 1)) {
+      err = "intensity stereo is not supported";
+      return false;
+    }
+    const size_t have = res_.size();
+    const uint8_t* md = f + off + side_bytes;
+    res_.insert(res_.end(), md, md + (h.bytes - off - side_bytes));
+    if ((size_t)si.main_data_begin > have) {  // the reservoir predates the stream's start
+      for (int ch = 0; ch < h.channels; ++ch) std::memset(out[ch], 0, sizeof(float) * 1152);
+      trim_reservoir();
+      return true;
+    }
+    Bits b{res_.data(), res_.size() * 8, (have - si.main_data_begin) * 8};
+    const int sr = h.rate_idx;
+    for (int gr = 0; gr < 2; ++gr) {
+      double xr[2][576];
+      for (int ch = 0; ch < h.channels; ++ch) {
+        const Granule& g = si.g[gr][ch];
+        const size_t start = b.pos;
+        if (g.block_type == 2 && !g.wsf) {
+          err = "bad block type";
+          return false;
+        }
+        read_scalefactors(b, g, si.scfsi[ch], gr, ch);
+        int is[576];
+        if (!huffman(b, g, sr, start + g.part23, is, err)) return false;
+        b.pos = start + g.part23;
+        requantize(g, sr, ch, is, xr[ch]);
+      }
+      if (h.mode == 1 && (h.mode_ext & 2)) {  // mid / side
+        const double r = 1.0 / std::sqrt(2.0);
+        for (int i = 0; i < 576; ++i) {
+          const double m = xr[0][i], s = xr[1][i];
+          xr[0][i] = (m + s) * r;
+          xr[1][i] = (m - s) * r;
+        }
+      }
+      for (int ch = 0; ch < h.channels; ++ch) {
+        const Granule& g = si.g[gr][ch];
+        reorder(g, sr, xr[ch]);
+        alias_reduce(g, xr[ch]);
+        double sub[32][18];
+        imdct(g, ch, xr[ch], sub);
+        synth(ch, sub, out[ch] + gr * 576);
+      }
+    }
+    trim_reservoir();
+    return true;
+  }
+
+ private:
+  void trim_reservoir() {
+    if (res_.size() > 4096) res_.erase(res_.begin(), res_.end() - 4096);  // main_data_begin <= 511
+  }
+
+  void read_scalefactors(Bits& b, const Granule& g, const int scfsi[4], int gr, int ch) {
+    const int s1 = kSlen[g.sfc][0], s2 = kSlen[g.sfc][1];
+    if (g.wsf && g.block_type == 2) {
+      int sfb0 = 0;
+      if (g.mixed) {
+        for (int sfb = 0; sfb < 8; ++sfb) sfl_[ch][sfb] = (int)b.get(s1);
+        sfb0 = 3;
+      }
+      for (int sfb = sfb0; sfb < 12; ++sfb)
+        for (int w = 0; w < 3; ++w) sfs_[ch][sfb][w] = (int)b.get(sfb < 6 ? s1 : s2);
+      for (int w = 0; w < 3; ++w) sfs_[ch][12][w] = 0;
+    } else {
+      static const int band[5] = {0, 6, 11, 16, 21};
+      for (int k = 0; k < 4; ++k)
+        if (gr == 0 || !scfsi[k])
+          for (int sfb = band[k]; sfb < band[k + 1]; ++sfb) sfl_[ch][sfb] = (int)b.get(k < 2 ? s1 : s2);
+      sfl_[ch][21] = 0;
+    }
+  }
+
+  bool huffman(Bits& b, const Granule& g, int sr, size_t end, int* is, std::string& err) {
+    std::memset(is, 0, sizeof(int) * 576);
+    const int bv = std::min(g.big_values * 2, 576);
+    int r1, r2;
+    if (g.wsf && g.block_type == 2) {
+      r1 = 36;
+      r2 = 576;
+    } else {
+      r1 = kSfbL[sr][std::min(g.r0 + 1, 22)];
+      r2 = kSfbL[sr][std::min(g.r0 + g.r1 + 2, 22)];
+    }
+    r1 = std::min(r1, bv);
+    r2 = std::min(r2, bv);
+    const Trees& T = trees();
+    int i = 0;
+    for (; i < bv; i += 2) {
+      const int tsel = g.table[i < r1 ? 0 : i < r2 ? 1 : 2];
+      if (tsel == 4 || tsel == 14) {
+        err = "invalid Huffman table";
+        return false;
+      }
+      if (tsel == 0) continue;
+      const int book = tsel < 16 ? tsel : tsel < 24 ? 16 : 24;
+      const Tree& t = book == 16 ? t16() : book == 24 ? t24() : T.big[book];
+      const int dim = book >= 13 ? 16 : kBooks[book].dim;
+      const int v = tree_decode(t, b);
+      if (v < 0) {
+        err = "corrupt Huffman data";
+        return false;
+      }
+      int x = v / dim, y = v % dim;
+      const int lb = kLinbits[tsel];
+      if (lb && x == 15) x += (int)b.get(lb);
+      if (x && b.bit()) x = -x;
+      if (lb && y == 15) y += (int)b.get(lb);
+      if (y && b.bit()) y = -y;
+      is[i] = x;
+      is[i + 1] = y;
+    }
+    // count1 region: quadruples until the granule's bits end
+    while (i + 4 <= 576 && b.pos < end) {
+      int q;
+      if (g.c1table) q = 15 - (int)b.get(4);
+      else q = tree_decode(T.quad_a, b);
+      if (q < 0) {
+        err = "corrupt count1 data";
+        return false;
+      }
+      int val[4] = {(q >> 3) & 1, (q >> 2) & 1, (q >> 1) & 1, q & 1};
+      for (int k = 0; k < 4; ++k)
+        if (val[k] && b.bit()) val[k] = -1;
+      if (b.pos > end) break;  // the last quadruple ran past the granule: dropped
+      for (int k = 0; k < 4; ++k) is[i + k] = val[k];
+      i += 4;
+    }
+    ++stats_[0];
+    if (b.pos == end) ++stats_[1];
+    if (b.pos > end && i <= bv) {
+      err = "Huffman data overran part2_3_length";
+      return false;
+    }
+    return true;
+  }
+
+  static const Tree& t16() {
+    static Tree t = [] {
+      Tree x;
+      x.build(kH16c, kH16l, 256);
+      return x;
+    }();
+    return t;
+  }
+  static const Tree& t24() {
+    static Tree t = [] {
+      Tree x;
+      x.build(kH24c, kH24l, 256);
+      return x;
+    }();
+    return t;
+  }
+
+  void requantize(const Granule& g, int sr, int ch, const int* is, double* xr) {
+    const double gain = std::pow(2.0, 0.25 * (g.global_gain - 210));
+    const double sfm = 0.5 * (1 + g.sfs);
+    auto pow43 = [](int v) { return v >= 0 ? std::pow((double)v, 4.0 / 3.0) : -std::pow((double)-v, 4.0 / 3.0); };
+    int i = 0;
+    if (!(g.wsf && g.block_type == 2) || g.mixed) {  // long bands (all, or the first 36 samples of a mixed block)
+      const int lend = (g.wsf && g.block_type == 2) ? 36 : 576;
+      for (int sfb = 0; sfb < 22 && i < lend; ++sfb) {
+        const int e = std::min(kSfbL[sr][sfb + 1], lend);
+        const double f = gain * std::pow(2.0, -sfm * (sfl_[ch][sfb] + g.preflag * kPretab[sfb]));
+        for (; i < e; ++i) xr[i] = is[i] ? pow43(is[i]) * f : 0.0;
+      }
+    }
+    if (g.wsf && g.block_type == 2) {
+      for (int sfb = g.mixed ? 3 : 0; sfb < 13; ++sfb) {
+        const int width = kSfbS[sr][sfb + 1] - kSfbS[sr][sfb];
+        for (int w = 0; w < 3; ++w) {
+          const double f = std::pow(2.0, 0.25 * (g.global_gain - 210 - 8 * g.sbg[w])) *
+                           std::pow(2.0, -sfm * sfs_[ch][sfb][w]);
+          for (int k = 0; k < width; ++k, ++i) xr[i] = is[i] ? pow43(is[i]) * f : 0.0;
+        }
+      }
+    }
+  }
+
+  void reorder(const Granule& g, int sr, double* xr) {
+    if (!(g.wsf && g.block_type == 2)) return;
+    double tmp[576];
+    for (int sfb = g.mixed ? 3 : 0; sfb < 13; ++sfb) {
+      const int start = kSfbS[sr][sfb] * 3, width = kSfbS[sr][sfb + 1] - kSfbS[sr][sfb];
+      for (int w = 0; w < 3; ++w)
+        for (int k = 0; k < width; ++k) tmp[start + 3 * k + w] = xr[start + w * width + k];
+    }
+    const int from = g.mixed ? 36 : 0;
+    std::memcpy(xr + from, tmp + from, sizeof(double) * (576 - from));
+  }
+
+  void alias_reduce(const Granule& g, double* xr) {
+    int sbs = 32;
+    if (g.wsf && g.block_type == 2) sbs = g.mixed ? 2 : 0;
+    for (int sb = 1; sb < sbs; ++sb)
+      for (int i = 0; i < 8; ++i) {
+        const double bu = xr[18 * sb - 1 - i], bd = xr[18 * sb + i];
+        xr[18 * sb - 1 - i] = bu * cs_[i] - bd * ca_[i];
+        xr[18 * sb + i] = bd * cs_[i] + bu * ca_[i];
+      }
+  }
+
+  void imdct(const Granule& g, int ch, const double* xr, double sub[32][18]) {
+    for (int sb = 0; sb < 32; ++sb) {
+      const double* X = xr + 18 * sb;
+      double y[36];
+      const bool short_blk = g.wsf && g.block_type == 2 && !(g.mixed && sb < 2);
+      if (!short_blk) {
+        const int bt = (g.wsf && g.block_type == 2) ? 0 : g.block_type;  // mixed: long part, normal window
+        for (int i = 0; i < 36; ++i) {
+          double s = 0;
+          for (int k = 0; k < 18; ++k) s += X[k] * cos36_[i][k];
+          y[i] = s * win_[bt][i];
+        }
+      } else {
+        for (int i = 0; i < 36; ++i) y[i] = 0;
+        for (int w = 0; w < 3; ++w)
+          for (int i = 0; i < 12; ++i) {
+            double s = 0;
+            for (int k = 0; k < 6; ++k) s += X[3 * k + w] * cos12_[i][k];
+            y[6 + 6 * w + i] += s * win_[2][i];
+          }
+      }
+      for (int i = 0; i < 18; ++i) {
+        double v = y[i] + overlap_[ch][sb][i];
+        overlap_[ch][sb][i] = y[i + 18];
+        if ((sb & 1) && (i & 1)) v = -v;  // frequency inversion
+        sub[sb][i] = v;
+      }
+    }
+  }
+
+  void synth(int ch, const double sub[32][18], float* out) {
+    double* V = v_[ch];
+    for (int t = 0; t < 18; ++t) {
+      std::memmove(V + 64, V, sizeof(double) * (1024 - 64));
+      for (int i = 0; i < 64; ++i) {
+        double s = 0;
+        for (int k = 0; k < 32; ++k) s += n_[i][k] * sub[k][t];
+        V[i] = s;
+      }
+      for (int j = 0; j < 32; ++j) {
+        double s = 0;
+        for (int i = 0; i < 8; ++i) {
+          s += V[128 * i + j] * dwin_[64 * i + j];
+          s += V[128 * i + 96 + j] * dwin_[64 * i + 32 + j];
+        }
+        out[32 * t + j] = (float)s;
+      }
+    }
+  }
+
+  std::vector<uint8_t> res_;
+
+ public:
+  long long stats_[2] = {0, 0};  // granules decoded, granules whose Huffman data ended exactly at part2_3_length
+
+ private:
+  int sfl_[2][22] = {};
+  int sfs_[2][13][3] = {};
+  double overlap_[2][32][18];
+  double v_[2][1024];
+  double n_[64][32];
+  double dwin_[512];
+  double cos36_[36][18], cos12_[12][6], win_[4][36];
+  double cs_[8], ca_[8];
+};
+
+struct Stream {
+  size_t first = 0;         // offset of the first audio frame
+  int channels = 0, rate = 0;
+  long long frames = 0;     // audio frames
+  long long skip = 0, total = -1;  // gapless: leading samples to drop, samples to keep (-1: all)
+};
+
+bool scan(const uint8_t* d, size_t n, Stream& s, std::string& err) {
+  size_t i = 0;
+  if (n >= 10 && d[0] == 'I' && d[1] == 'D' && d[2] == '3')
+    i = 10 + ((size_t)(d[6] & 127) << 21 | (size_t)(d[7] & 127) << 14 | (size_t)(d[8] & 127) << 7 | (d[9] & 127));
+  Header h;
+  while (i + 4 <= n && !parse_header(d + i, h)) ++i;
+  if (i + 4 > n) {
+    err = "no MPEG-1 Layer III frame found";
+    return false;
+  }
+  s.first = i;
+  s.channels = h.channels;
+  s.rate = kRate[h.rate_idx];
+  // Xing / Info tag in the first frame: not audio; LAME's tag carries the encoder delay and padding
+  const int side = h.channels == 1 ? 17 : 32;
+  const size_t tag = i + 4 + (h.protect ? 2 : 0) + side;
+  long long xing_frames = -1;
+  if (tag + 8 <= n && (std::memcmp(d + tag, "Xing", 4) == 0 || std::memcmp(d + tag, "Info", 4) == 0)) {
+    const uint32_t flags = (uint32_t)d[tag + 4] << 24 | (uint32_t)d[tag + 5] << 16 | (uint32_t)d[tag + 6] << 8 | d[tag + 7];
+    size_t q = tag + 8;
+    if ((flags & 1) && q + 4 <= n) xing_frames = (long long)d[q] << 24 | d[q + 1] << 16 | d[q + 2] << 8 | d[q + 3];
+    q += (flags & 1 ? 4 : 0) + (flags & 2 ? 4 : 0) + (flags & 4 ? 100 : 0) + (flags & 8 ? 4 : 0);
+    if (q + 24 <= n && std::memcmp(d + q, "LAME", 4) == 0) {
+      const int delay = d[q + 21] << 4 | d[q + 22] >> 4, pad = (d[q + 22] & 15) << 8 | d[q + 23];
+      s.skip = delay + kDecoderDelay;
+      if (xing_frames >= 0) s.total = xing_frames * 1152 - delay - pad;
+    }
+    s.first = i + h.bytes;
+  }
+  for (size_t p = s.first; p + 4 <= n;) {
+    Header g;
+    if (!parse_header(d + p, g) || p + g.bytes > n) break;
+    ++s.frames;
+    p += g.bytes;
+  }
+  if (s.total < 0) {
+    s.skip = 0;
+    s.total = s.frames * 1152;
+  }
+  s.total = std::max(0LL, std::min(s.total, s.frames * 1152 - s.skip));
+  return true;
+}
+
+thread_local std::string g_mp3_err;
+thread_local long long g_mp3_stats[2];
+
+}  // namespace
+
+extern "C" int dcx_mp3_info(const uint8_t* data, size_t nbytes, int64_t* samples, int32_t* sample_rate,
+                            int32_t* channels) {
+  if (!data || !samples || !sample_rate || !channels) return DCX_ERR_INVALID_ARG;
+  Stream s;
+  if (!scan(data, nbytes, s, g_mp3_err)) return DCX_ERR_INVALID_ARG;
+  *samples = s.total;
+  *sample_rate = s.rate;
+  *channels = s.channels;
+  return DCX_OK;
+}
+
+extern "C" int dcx_mp3_decode(const uint8_t* data, size_t nbytes, float* out, int64_t capacity) {
+  if (!data || !out) return DCX_ERR_INVALID_ARG;
+  g_mp3_stats[0] = g_mp3_stats[1] = 0;
+  Stream s;
+  if (!scan(data, nbytes, s, g_mp3_err)) return DCX_ERR_INVALID_ARG;
+  if (capacity < s.total) {
+    g_mp3_err = "output capacity below dcx_mp3_info's sample count";
+    return DCX_ERR_INVALID_ARG;
+  }
+  Decoder dec;
+  std::vector<float> pcm[2];
+  for (int ch = 0; ch < s.channels; ++ch) pcm[ch].assign(1152, 0.f);
+  long long produced = 0;  // decoded samples per channel so far
+  size_t p = s.first;
+  for (long long f = 0; f < s.frames; ++f) {
+    Header h;
+    if (!parse_header(data + p, h)) break;
+    float* o[2] = {pcm[0].data(), s.channels > 1 ? pcm[1].data() : nullptr};
+    if (h.channels != s.channels || kRate[h.rate_idx] != s.rate) {
+      g_mp3_err = "channel count or sample rate changes inside the stream";
+      return DCX_ERR_INVALID_ARG;
+    }
+    if (!dec.frame(data + p, h, o, g_mp3_err)) return DCX_ERR_INVALID_ARG;
+    for (int i = 0; i < 1152; ++i, ++produced) {
+      const long long k = produced - s.skip;
+      if (k < 0 || k >= s.total) continue;
+      for (int ch = 0; ch < s.channels; ++ch) out[(long long)ch * s.total + k] = pcm[ch][i];
+    }
+    p += h.bytes;
+  }
+  g_mp3_stats[0] = dec.stats_[0];
+  g_mp3_stats[1] = dec.stats_[1];
+  return DCX_OK;
+}
+
+extern "C" int dcx_mp3_stats(int64_t* granules, int64_t* exact) {
+  if (!granules || !exact) return DCX_ERR_INVALID_ARG;
+  *granules = g_mp3_stats[0];
+  *exact = g_mp3_stats[1];
+  return DCX_OK;
+}
+
+extern "C" const char* dcx_mp3_last_error(void) { return g_mp3_err.c_str(); }

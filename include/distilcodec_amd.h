@@ -138,6 +138,19 @@ int dcx_encode_decode(dcx_codec* h, const float* audio, int32_t batch, int64_t n
 int dcx_resample_poly(const float* x, int32_t batch, int64_t n_in, int64_t x_stride, const double* h, int32_t h_len,
                       int32_t up, int32_t down, int64_t pre, float* y, int64_t n_out, int64_t y_stride, void* stream);
 
+/* MP3 input (host code, no device involved): an MPEG-1 Layer III decoder replacing librosa.load's MP3
+ * path (meldataset.py:18-20, distil_codec.py:667; C1's test.mp3, README.md:116), with Xing/LAME
+ * gapless trimming (encoder delay + 529 decoder-delay samples skipped, encoder padding dropped).
+ * dcx_mp3_info: samples per channel, sample rate, channels.  dcx_mp3_decode: channel-major float
+ * samples out[ch][samples] (capacity = samples per channel available).  MPEG-2/2.5, free format and
+ * intensity stereo return DCX_ERR_INVALID_ARG; dcx_mp3_last_error() has the text (per thread).
+ * dcx_mp3_stats: granules of the last decode, and how many of them ended their Huffman data exactly
+ * at part2_3_length (a check on the code books). */
+int dcx_mp3_info(const uint8_t* data, size_t nbytes, int64_t* samples, int32_t* sample_rate, int32_t* channels);
+int dcx_mp3_decode(const uint8_t* data, size_t nbytes, float* out, int64_t capacity);
+const char* dcx_mp3_last_error(void);
+int dcx_mp3_stats(int64_t* granules, int64_t* exact);
+
 /* Batched 2-D transpose [B][R][C] -> [B][C][R] (channels-first <-> channels-last bridge). */
 int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int64_t cols, void* stream);
 

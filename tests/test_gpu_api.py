@@ -184,3 +184,34 @@ def test_too_short_clip_raises(codec):
         R.log_mel(audio)
     with pytest.raises(ValueError, match="too short"):
         codec._engine().encode_decode(audio.cuda())
+
+
+def test_c1_reference_demo_mp3(codec, state, cfg):
+    """BASELINE configs[0] (C1): the reference's demo on its own test.mp3 (README.md:103-133):
+    MP3 decode (host, csrc/dcx_mp3.cpp) -> 44.1 -> 24 kHz resampling (GPU) -> encode.  The demo's
+    bf16 tokens have the right count and offset; the fp32 path-input encode of the same file equals
+    the CPU oracle run on the oracle's own resampling of the decoded samples (decisive codes exact,
+    waveform >= 80 dB).  MP3 decoding itself is pinned by properties only (tests/test_mp3.py)."""
+    import os
+
+    from distilcodec_nabeel_amd import demo_for_generate_audio_codes, mp3
+    from oracle import reference_cpu as R
+    from oracle import resample_cpu as RS
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "test.mp3")
+    x, sr = mp3.read_mp3(path)
+    y = RS.resample(x[:, 0].astype(np.float64), sr, 24000).astype(np.float32)
+    audio, _ = R.pad_batch([y])
+    T = codec._engine().num_frames(audio.shape[1])
+    toks = demo_for_generate_audio_codes(codec, path)
+    assert len(toks) == T and min(toks) >= codec.tokens_id_offset
+    ret, _, hop = codec.encode([path])
+    assert hop == [len(y) // 256]
+    ref = R.encode_decode(audio, state, cfg)
+    rc = ref["codes"][0, :, :, 0].numpy()
+    best, second, _ = R.top2_gap_fp64(ref["x_pjt_in"], R.codebook(state["quantizer"]))
+    dec = (((second - best) / best) > 1e-4).numpy().reshape(rc.shape)
+    codes = ret.codes[0, :, :, 0]
+    check_codes(codes, rc, dec)
+    wav = codec.decode_from_codes(codes[0].tolist(), minus_token_offset=False)
+    check_wave(codec._engine(), codes, rc, wav[:, 0], ref["wav"][:, 0].numpy(), 80)
