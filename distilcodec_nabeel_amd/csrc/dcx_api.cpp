@@ -37,6 +37,7 @@ struct HostTensor {
 struct ConvW {
   float* w = nullptr;
   unsigned short* w6 = nullptr;  // bf16 3-plane split, x6 kernel layout
+  unsigned short* wc = nullptr;  // 1x1 convs: hi plane only, [Cin/32][Cout][32] (bf16 mode, conv_gemm_bf16dm)
   float* b = nullptr;
   int cin = 0, cout = 0, taps = 1, phases = 1, in_step = 1, out_mul = 1;
   int in_base[dcx::kMaxPhases] = {0};
@@ -105,11 +106,15 @@ struct dcx_codec {
   float emax = 0.f, e2max = 0.f;  // largest codebook row norm / squared norm (prefilter bound)
   int* vq_stats = nullptr;        // [rows rescored, codes rescored] (dcx_vq_rescore_stats)
   unsigned short* codebook6 = nullptr;
+  unsigned short* codebook_bk = nullptr;  // hi/mid per K32 step (bf16-mode prefilter, vq_prefilter_bk)
   unsigned short* ptable6 = nullptr;  // decode table as activation planes (x6 mode gathers)
   int gemm_mode = DCX_GEMM_X6;
   // fused ResBlock pairs for the C = 32 / 64 generator stages (conv_res_pair); DCX_NO_RESPAIR=1 at
   // dcx_create keeps the per-conv launches (A/B comparisons)
   bool res_pair = true;
+  // compact bf16 activations between bf16-mode producers and conv_gemm_bf16dm / vq_prefilter_bk;
+  // DCX_NO_COMPACT=1 at dcx_create keeps the planes layout (A/B comparisons, same bits)
+  bool compact = true;
 
   ConvW conv_pre;
   ConvW ups[8];
@@ -323,6 +328,15 @@ struct Builder {
           }
     return upload16(out);
   }
+  // fp32 packed [cout][cin] (one tap, one phase) -> [cin/32][cout][32] bf16 hi (conv_gemm_bf16dm)
+  unsigned short* compact_pack(const std::vector<float>& pk, int cout, int cin) {
+    if (bad() || dry) return nullptr;
+    std::vector<unsigned short> out((size_t)cout * cin);
+    for (int st = 0; st < cin / 32; ++st)
+      for (int o = 0; o < cout; ++o)
+        for (int j = 0; j < 32; ++j) out[((size_t)st * cout + o) * 32 + j] = bf16_rne(pk[(size_t)o * cin + st * 32 + j]);
+    return upload16(out);
+  }
   float* alloc(size_t n) {
     if (bad() || dry) return nullptr;
     void* p = nullptr;
@@ -375,6 +389,7 @@ struct Builder {
         for (int j = 0; j < k; ++j) pk[((size_t)o * k + j) * cin + i] = w.data[((size_t)o * cin + i) * k + j];
     c.w = upload(pk);
     if (cin % 16 == 0) c.w6 = split_pack(pk, 1, cout, k, cin);
+    if (k == 1 && cin % 32 == 0) c.wc = compact_pack(pk, cout, cin);
     if (has_bias) c.b = vec(prefix + ".bias", cout);
     return c;
   }
@@ -477,16 +492,20 @@ int max_gen_width(const dcx_config& c) {  // max over generator layers of channe
 // launches
 // ----------------------------------------------------------------------------------------
 // An activation tensor [rows][C]: fp32 and/or x6 planes ([rows][C/8][3][8] bf16, dcx_planes.h).
+// c1: p holds the compact bf16 layout ([rows][C] hi only; bf16 mode, consumers conv_gemm_bf16dm /
+// vq_prefilter_bk) instead of planes.
 struct Act {
   float* f = nullptr;
   unsigned short* p = nullptr;
+  bool c1 = false;
 };
 struct CAct {
   const float* f = nullptr;
   const unsigned short* p = nullptr;
+  bool c1 = false;
   CAct() = default;
-  CAct(const float* f_, const unsigned short* p_) : f(f_), p(p_) {}
-  CAct(const Act& a) : f(a.f), p(a.p) {}
+  CAct(const float* f_, const unsigned short* p_, bool c1_ = false) : f(f_), p(p_), c1(c1_) {}
+  CAct(const Act& a) : f(a.f), p(a.p), c1(a.c1) {}
 };
 
 // planes layout for every GEMM operand (x6 and bf16 modes)
@@ -508,6 +527,7 @@ struct ConvCall {
   float* y2 = nullptr;           // silu(v), fp32
   unsigned short* y6 = nullptr;  // planes of v
   unsigned short* y6s = nullptr; // planes of silu(v)
+  bool y6c = false;              // y6 in the compact bf16 layout
   float* macc = nullptr;
   const float* res = nullptr;
   const float* gamma = nullptr;
@@ -515,7 +535,7 @@ struct ConvCall {
   bool exact = false;  // keep x6 arithmetic in bf16 mode (the reference's fp32 mel front end)
   bool silu_in = false;  // fp32 input: the conv consumes silu(x) (applied while staging)
   void silu_to(const Act& a) { y2 = a.f; y6s = a.p; }
-  void out_to(const Act& a) { y = a.f; y6 = a.p; }
+  void out_to(const Act& a) { y = a.f; y6 = a.p; y6c = a.c1; }
 };
 
 // Planes-mode convs with Cout <= 64, Cin <= 128 and a tap halo take an fp32 input (split while
@@ -560,7 +580,18 @@ int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32,
   p.nprod = one ? 1 : 6;
   p.round_bf16 = one;
   p.silu_in = c.silu_in;
+  p.x_compact = x6 && c.x.p && c.x.c1;
+  p.y_compact = c.y6 && c.y6c;
+  p.wc = one && h->compact ? w.wc : nullptr;
+  if ((p.x_compact || p.y_compact) && !one) return fail(h, DCX_ERR_STATE, "internal: compact layout outside bf16 mode");
   return DCX_OK;
+}
+
+// Whether a one-tap conv over `rows` rows runs on conv_gemm_bf16dm in this handle's mode, so its
+// producer may write the compact bf16 layout (2 bytes per element instead of 6).
+bool takes_compact(const dcx_codec* h, const ConvW& w, long long rows) {
+  return h->compact && h->gemm_mode == DCX_GEMM_BF16 && w.wc && w.taps == 1 && w.phases == 1 && w.in_base[0] == 0 &&
+         rows < (1LL << 31) && dcx::bf16dm_takes(w.cin, w.cout, (int)rows, w.cin, 1);
 }
 
 // algorithmic FLOPs and bytes of one conv (profiling)
@@ -634,25 +665,30 @@ ConvCall framed(CAct x, int B, int L, int C) {
     ps_.done(name, flops, bytes);              \
   } while (0)
 
-// fp32 -> planes for a tensor handed in by the caller (x6 mode only).
-int ensure_planes(dcx_codec* h, CAct& a, long long rows, int C, Bump& ws, hipStream_t s) {
+// fp32 -> planes (or, with compact, bf16) for a tensor handed in by the caller (x6 / bf16 modes).
+int ensure_planes(dcx_codec* h, CAct& a, long long rows, int C, Bump& ws, hipStream_t s, bool compact = false) {
   if (!x6_mode(h) || a.p) return DCX_OK;
   unsigned short* p = ws.u16((size_t)rows * C * 3);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small");
-  LAUNCH(h, s, "split_planes", 0, 10.0 * rows * C, dcx::launch_split_planes(a.f, p, rows, C, s));
+  LAUNCH(h, s, "split_planes", 0, (compact ? 6.0 : 10.0) * rows * C,
+         dcx::launch_split_planes(a.f, p, rows, C, compact ? 1 : 0, s));
   a.p = p;
+  a.c1 = compact;
   return DCX_OK;
 }
 
-// ConvNeXtBlock in place on x [B][T][C] (fp32 residual stream); out6: optional planes of the
-// block output for a following conv.  ln: [M][C], hid: [M][4C] conv-input scratch.
+// ConvNeXtBlock in place on x [B][T][C] (fp32 residual stream); out6: optional planes (compact
+// with out6c) of the block output for a following conv.  ln: [M][C], hid: [M][4C] conv-input
+// scratch, written compact where their consumer takes it (bf16 mode).
 int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, int B, int T, Act ln, Act hid,
-              hipStream_t s) {
+              hipStream_t s, bool out6c = false) {
   const long long M = (long long)B * T;
   const int C = bw.C;
+  ln.c1 = ln.p && takes_compact(h, bw.pw1, M);
+  hid.c1 = hid.p && takes_compact(h, bw.pw2, M);
   LAUNCH(h, s, "dwconv_ln", 14.0 * M * C, 8.0 * M * C,
-         dcx::launch_dwconv_ln(x, ln.f, ln.p, bw.dww, bw.dwb, bw.ln.w, bw.ln.b, B, T, C, s));
+         dcx::launch_dwconv_ln(x, ln.f, ln.p, ln.c1 ? 1 : 0, bw.dww, bw.dwb, bw.ln.w, bw.ln.b, B, T, C, s));
   ConvCall c1 = pointwise(ln, M);
   c1.out_to(hid);
   c1.epi = dcx::EPI_GELU;
@@ -660,6 +696,7 @@ int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, in
   ConvCall c2 = pointwise(hid, M);
   c2.y = x;
   c2.y6 = out6;
+  c2.y6c = out6 && out6c;
   c2.res = x;
   c2.gamma = bw.gamma;
   c2.epi = dcx::EPI_GAMMA_RES;
@@ -669,7 +706,7 @@ int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, in
 
 int run_ln(dcx_codec* h, const LnW& l, const float* x, Act y, long long rows, hipStream_t s) {
   LAUNCH(h, s, "ln_rows", 8.0 * rows * l.C, 8.0 * rows * l.C,
-         dcx::launch_ln_rows(x, y.f, y.p, l.w, l.b, rows, l.C, 1e-6f, 1, s));
+         dcx::launch_ln_rows(x, y.f, y.p, y.p && y.c1 ? 1 : 0, l.w, l.b, rows, l.C, 1e-6f, 1, s));
   return DCX_OK;
 }
 
@@ -718,6 +755,7 @@ int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipSt
   RUN(run_ln(h, h->stem_ln, xa, Act{xb, nullptr}, M, s));
   for (int i = 0; i < 4; ++i) {
     if (i > 0) {
+      ln.c1 = ln.p && takes_compact(h, h->ds_conv[i], M);
       RUN(run_ln(h, h->ds_ln[i], xb, ln, M, s));
       ConvCall cd = pointwise(ln, M);
       cd.y = xb;
@@ -736,7 +774,8 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   const int D = c.vq_dim, CD = c.codebook_dim, NC = c.codebook_size;
   const bool x6 = x6_mode(h);
   const int ntiles = x6 ? dcx::vq_prefilter_ntiles(NC, CD) : dcx::vq_argmin_ntiles(NC);
-  RUN(ensure_planes(h, feat, M, D, ws, s));
+  RUN(ensure_planes(h, feat, M, D, ws, s, takes_compact(h, h->vq_down, M)));
+  if (feat.c1 && !takes_compact(h, h->vq_down, M)) return fail(h, DCX_ERR_STATE, "internal: compact features");
   float* X = ws.f((size_t)M * D);
   unsigned short* X6 = x6 ? ws.u16((size_t)M * D * 3) : nullptr;
   Act ln = conv_input(h, ws, (size_t)M * D);
@@ -753,10 +792,14 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   ConvCall cd = pointwise(feat, M);
   cd.y = X;
   RUN(run_conv(h, h->vq_down, cd, s));
-  RUN(run_block(h, h->vq_down_blk, X, X6, B, T, ln, hid, s));
-  ConvCall cp = pointwise(CAct(X, X6), M);
+  const bool x6c = X6 && takes_compact(h, h->vq_pin, M);
+  // bf16 mode: x_pjt_in compact for vq_prefilter_bk (the repacked codebook exists iff it takes the shape)
+  const bool p6c = P6 && h->compact && h->gemm_mode == DCX_GEMM_BF16 && h->codebook_bk;
+  RUN(run_block(h, h->vq_down_blk, X, X6, B, T, ln, hid, s, x6c));
+  ConvCall cp = pointwise(CAct(X, X6, x6c), M);
   cp.y = P;
   cp.y6 = P6;
+  cp.y6c = p6c;
   RUN(run_conv(h, h->vq_pin, cp, s));
   LAUNCH(h, s, "row_sqnorm", 2.0 * M * CD, 4.0 * M * CD, dcx::launch_row_sqnorm(P, M, CD, x2, s));
   {
@@ -764,6 +807,8 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
     p.x = P; p.x6 = P6; p.w = h->codebook; p.w6 = x6 ? h->codebook6 : nullptr;
     p.Cin = CD; p.Cout = NC; p.ldx = CD; p.taps = 1; p.in_step = 1; p.out_mul = 1;
     p.x2 = x2; p.e2 = h->e2; p.part_val = pv; p.part_idx = pi; p.part_val2 = pv2;
+    p.x_compact = p6c;
+    p.wc = p6c ? h->codebook_bk : nullptr;
     ProfScope ps(h, s);
     const char* kname = "vq";
     if (x6) {
@@ -988,6 +1033,7 @@ int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int3
   const long long M = (long long)B * T;
   Act mel = conv_input(h, ws, (size_t)M * c.n_mels);
   Act feat = conv_input(h, ws, (size_t)M * c.enc_dims[3]);
+  feat.c1 = feat.p && takes_compact(h, h->vq_down, M);  // written by the encoder's final LayerNorm
   Act z;
   z.f = ws.f((size_t)M * c.vq_dim);
   if (x6_mode(h)) z.p = ws.u16((size_t)M * c.vq_dim * 3);
@@ -1096,6 +1142,8 @@ int dcx_create(const dcx_config* cfg, dcx_codec** out) {
   hipGetDevice(&h->device);
   const char* nrp = std::getenv("DCX_NO_RESPAIR");
   h->res_pair = !(nrp && nrp[0] == '1');
+  const char* ncp = std::getenv("DCX_NO_COMPACT");
+  h->compact = !(ncp && ncp[0] == '1');
   *out = h;
   return DCX_OK;
 }
@@ -1189,6 +1237,13 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
       h->codebook = B.upload(emb->data);
       h->codebook6 = B.split_pack(emb->data, 1, NC, 1, CD);
       h->e2 = B.upload(e2);
+      if (dcx::vq_bk_takes(NC, CD)) {
+        h->codebook_bk = (unsigned short*)B.alloc((size_t)NC * CD);  // NC * CD * 2 bf16 (hi, mid)
+        if (!B.bad() && !B.dry &&
+            (dcx::launch_repack_codebook_bk(h->codebook6, NC, CD, h->codebook_bk, 0) != hipSuccess ||
+             hipDeviceSynchronize() != hipSuccess))
+          return fail(h, DCX_ERR_HIP, "bf16 codebook repack failed");
+      }
     }
     // decode table: project_out applied to every code once, E * W_out^T + b_out
     h->ptable = B.alloc((size_t)NC * D);
@@ -1199,7 +1254,7 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
       cp.y = h->ptable;
       int rc = run_conv(h, pout, cp, 0, /*force_f32=*/true);
       if (rc != DCX_OK) return rc;
-      if (dcx::launch_split_planes(h->ptable, h->ptable6, NC, D, 0) != hipSuccess ||
+      if (dcx::launch_split_planes(h->ptable, h->ptable6, NC, D, 0, 0) != hipSuccess ||
           hipDeviceSynchronize() != hipSuccess)
         return fail(h, DCX_ERR_HIP, "decode-table build failed");
     }
@@ -1408,7 +1463,7 @@ int dcx_conv_forward(dcx_conv* c, int32_t gemm_mode, const float* x, int32_t bat
       if (hipMalloc(&c->planes, need * sizeof(unsigned short)) != hipSuccess) return DCX_ERR_OOM;
       c->planes_cap = need;
     }
-    if (dcx::launch_split_planes(x, c->planes, (long long)batch * lin, c->w.cin, s) != hipSuccess) return DCX_ERR_HIP;
+    if (dcx::launch_split_planes(x, c->planes, (long long)batch * lin, c->w.cin, 0, s) != hipSuccess) return DCX_ERR_HIP;
     xa.p = c->planes;
   }
   ConvCall cc = framed(xa, batch, (int)lin, c->w.cin);

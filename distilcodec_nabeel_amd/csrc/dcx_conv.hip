@@ -168,7 +168,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
   const int wm = wave / WN, wn = wave % WN;
   const int lrow = lane & 31, rhalf = 4 * (lane >> 5);
   const long long ob = (long long)b * p.y_bstride;
-  unsigned short* y6 = p.y6 ? p.y6 + ob * 3 : nullptr;
+  unsigned short* y6 = p.y6 ? p.y6 + ob * (p.y_compact ? 1 : 3) : nullptr;
   unsigned short* y6s = p.y6s ? p.y6s + ob * 3 : nullptr;
   static_assert(NT % (BN / 4) == 0, "each thread keeps one 4-channel group");
   const int c4 = (tid % (BN / 4)) * 4, trow = tid / (BN / 4), co = co0 + c4;
@@ -265,7 +265,10 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
         x = (m[k] + x) / 3.0f;
       }
       if (p.y) *reinterpret_cast<f32x4*>(p.y + o) = x;
-      if (y6) store_planes4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
+      if (y6) {
+        if (p.y_compact) store_bf16x4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
+        else store_planes4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
+      }
       if (p.y2 || y6s) {
         f32x4 sv;
 #pragma unroll
@@ -1991,36 +1994,44 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
   const int nsteps = p.Cin / 32;
-  const int arow = p.ldx * 6;
+  // input: planes (hi pieces at 48-byte strides, 6 bytes per element) or compact bf16 (x_compact:
+  // one contiguous 64-byte run per row and step); weights: planes w6 or compact wc likewise
+  const int xc = p.x_compact ? 1 : 3;
+  const int arow = p.ldx * 2 * xc, a_kq = 16 * xc, a_step = 64 * xc;
   const int row0 = q0 + p.in_base[ph];  // >= 0 for 1x1 convs; the descriptor covers the tile's rows
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.x6 + ((long long)b * p.x_bstride + (long long)row0 * p.ldx) * 3), 0,
+      (void*)(p.x6 + ((long long)b * p.x_bstride + (long long)row0 * p.ldx) * xc), 0,
       max(0, min(BM, p.Lin - row0)) * arow, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.w6 + (long long)ph * (p.Cin / 16) * p.Cout * 48), 0, (p.Cin / 16) * p.Cout * 96, 0x00020000);
+  const bool wc = p.wc != nullptr;
+  const __amdgpu_buffer_rsrc_t rw =
+      wc ? __builtin_amdgcn_make_buffer_rsrc((void*)(p.wc + (long long)ph * (p.Cin / 32) * p.Cout * 32), 0,
+                                             (p.Cin / 32) * p.Cout * 64, 0x00020000)
+         : __builtin_amdgcn_make_buffer_rsrc((void*)(p.w6 + (long long)ph * (p.Cin / 16) * p.Cout * 48), 0,
+                                             (p.Cin / 16) * p.Cout * 96, 0x00020000);
+  const int b_step = wc ? p.Cout * 64 : p.Cout * 192;
 
   // DMA pieces (bytes, step 0): unit u -> row (u / 64) * 16 + (u & 15), piece (u % 64) >> 4 = the
-  // 8-channel group kq; step s adds s * 192 (input) and s * Cout * 192 (weights: two K16 chunks)
+  // 8-channel group kq; step s adds s * a_step (input) and s * b_step (weights: two K16 chunks)
   int a_off[A_PW], b_off[B_PW];
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     const int u = (group * A_G + i * 4 + gw) * 64 + lane;
     const int r = (u >> 6) * 16 + (u & 15), kq = (u & 63) >> 4;
-    a_off[i] = r * arow + kq * 48;  // rows past Lin: out of range, zeros
+    a_off[i] = r * arow + kq * a_kq;  // rows past Lin: out of range, zeros
   }
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
     const int u = (group * B_G + i * 4 + gw) * 64 + lane;
     const int c = (u >> 6) * 16 + (u & 15), kq = (u & 63) >> 4;
-    b_off[i] = (kq >> 1) * p.Cout * 96 + (co0 + c) * 96 + (kq & 1) * 48;
+    b_off[i] = wc ? (co0 + c) * 64 + kq * 16 : (kq >> 1) * p.Cout * 96 + (co0 + c) * 96 + (kq & 1) * 48;
   }
   unsigned short* const a_dst = lds + (group * A_G + gw) * 512;
   unsigned short* const b_dst = lds + 3 * ABUF + (group * B_G + gw) * 512;
   auto dma_step = [&](int s, int slot) {
 #pragma unroll
-    for (int i = 0; i < A_PW; ++i) dma16(rx, a_dst + slot * ABUF + i * 2048, a_off[i] + s * 192, 0);
+    for (int i = 0; i < A_PW; ++i) dma16(rx, a_dst + slot * ABUF + i * 2048, a_off[i] + s * a_step, 0);
 #pragma unroll
-    for (int i = 0; i < B_PW; ++i) dma16(rw, b_dst + slot * BBUF + i * 2048, b_off[i], s * p.Cout * 192);
+    for (int i = 0; i < B_PW; ++i) dma16(rw, b_dst + slot * BBUF + i * 2048, b_off[i], s * b_step);
     return A_PW + B_PW;
   };
 
@@ -2482,6 +2493,158 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_dm(const ConvParams p) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// vq_prefilter_bk: the bf16-mode prefilter (x_pjt_in bf16-valued: x = hi) on K32 steps.
+//
+// vq_prefilter_dm in bf16 mode issued 16 MFMAs per segment against two barriers, staged x's mid
+// plane (zero) and read hi/mid pieces at 48-byte strides.  Here a step is K32 (two K16 chunks cc):
+// x arrives in the compact bf16 layout (one 64-byte run per row and step) and the codebook as
+// launch_repack_codebook_bk packs it (one 128-byte run of hi/mid pieces per code and step), so
+// every DMA instruction reads whole cache lines, and a segment issues 32 MFMAs:
+//   per cc: acc += x_h . e_m',  acc += x_h . e_h'   (v_mfma_f32_32x32x16_bf16)
+// the products of vq_prefilter_dm's bf16 mode, so the bound of launch_vq_prefilter holds as is.
+// Ring: 3 slots of 16 KiB (x) + 32 KiB (codebook), the ping-pong schedule of vq_prefilter_dm.
+// LDS images (lane-linear per DMA instruction, swizzle applied on the source):
+//   x:  64-byte rows, piece p = cc * 2 + hh in slot p ^ ((row >> 2) & 3);
+//   e: 128-byte rows, piece p = (cc * 2 + hh) * 2 + plane in slot p ^ ((code >> 1) & 7);
+// both conflict-free for the four lane groups of a ds_read_b128 (MI355X_MICROARCH.md §LDS).
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(512, 2) vq_prefilter_bk(const ConvParams p) {
+  constexpr int BM = 256, BN = 256, WN = 2;
+  constexpr int WR = BM / 4, WC = BN / 2, TM = WR / 32, TN = WC / 32;
+  constexpr int ARW = 32, BRW = 64;            // ushorts per LDS row
+  constexpr int A_G = BM * 4 / 64 / 2;         // DMA instructions per group per tile (x: 8)
+  constexpr int B_G = BN * 8 / 64 / 2;         // (codebook: 16)
+  constexpr int A_PW = A_G / 4, B_PW = B_G / 4;  // per wave
+  constexpr int ABUF = BM * ARW, BBUF = BN * BRW;
+  constexpr int LDS_US = 3 * ABUF + 3 * BBUF;  // 144 KiB
+  static_assert(A_G % 4 == 0 && B_G % 4 == 0 && LDS_US * 2 <= 160 * 1024, "tile shape");
+  __shared__ __attribute__((aligned(16))) unsigned short lds[LDS_US];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int group = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int wm = wave >> 1, wn = wave & 1;
+  // grouped order of vq_prefilter_dm: 16 row panels x 16 code tiles resident together
+  const int ntiles = p.Cout / BN, mtiles = (p.Lq + BM - 1) / BM;
+  const int bid = blockIdx.x, xc = bid & 7, l = (bid >> 3) & 31, sup = bid >> 8;
+  const int nsm = (mtiles + 15) >> 4;
+  const int mt = (sup % nsm) * 16 + (xc & 3) * 4 + (l & 3);
+  const int nt = (sup / nsm) * 16 + (xc >> 2) * 8 + (l >> 2);
+  if (mt >= mtiles) return;  // whole workgroup, before any barrier
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int nsteps = p.Cin / 32;
+  const int arow = p.ldx * 2;  // bytes per compact row
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.x6 + (long long)q0 * p.ldx), 0, min(BM, p.Lq - q0) * arow, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wc, 0, nsteps * p.Cout * 128, 0x00020000);
+
+  int a_off[A_PW], b_off[B_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int u = (group * A_G + i * 4 + gw) * 64 + lane;
+    const int row = u >> 2, pc = (u & 3) ^ ((row >> 2) & 3);
+    a_off[i] = row * arow + pc * 16;
+  }
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int u = (group * B_G + i * 4 + gw) * 64 + lane;
+    const int code = u >> 3, pc = (u & 7) ^ ((code >> 1) & 7);
+    b_off[i] = (co0 + code) * 128 + pc * 16;
+  }
+  unsigned short* const a_dst = lds + (group * A_G + gw) * 512;
+  unsigned short* const b_dst = lds + 3 * ABUF + (group * B_G + gw) * 512;
+  auto dma_step = [&](int c, int slot) {
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) dma16(rx, a_dst + slot * ABUF + i * 2048, a_off[i] + c * 64, 0);
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) dma16(rw, b_dst + slot * BBUF + i * 2048, b_off[i], c * p.Cout * 128);
+    return A_PW + B_PW;
+  };
+
+  const int lrow = lane & 31, h = lane >> 5;
+  s16x8 af[TM][2], bfr[TN][2][2];
+  auto readF = [&](int slot) {
+    const unsigned short* A = lds + slot * ABUF;
+    const unsigned short* Bs = lds + 3 * ABUF + slot * BBUF;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm * WR + i * 32 + lrow;
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+        af[i][cc] = *reinterpret_cast<const s16x8*>(A + r * ARW + (((cc * 2 + h) ^ ((r >> 2) & 3)) << 3));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WC + j * 32 + lrow;
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          bfr[j][cc][pl] = *reinterpret_cast<const s16x8*>(
+              Bs + col * BRW + (((((cc * 2 + h) * 2) + pl) ^ ((col >> 1) & 7)) << 3));
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  auto mfma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[i][cc]),
+                                                              __builtin_bit_cast(bf16x8, bfr[j][cc][1]), acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[i][cc]),
+                                                              __builtin_bit_cast(bf16x8, bfr[j][cc][0]), acc[i][j], 0, 0, 0);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto inc3 = [](int& slot) { slot = slot == 2 ? 0 : slot + 1; };
+
+  for (int t = 0; t < 3; ++t) dma_step(t, t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  seg_barrier();
+  if (group == 0) {
+    readF(0);
+    int rs = 1, ws = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      mfma();  // MFMA(s)
+      seg_barrier();
+      if (s + 1 < nsteps) readF(rs);  // MEM0(s): fragments of step s + 1, issue step s + 3
+      int n = 0;
+      if (s + 3 < nsteps) n = dma_step(s + 3, ws);
+      wait_dma(n);
+      seg_barrier();
+      inc3(rs);
+      inc3(ws);
+    }
+  } else {
+    int rs = 0, ws = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      readF(rs);  // MEM1(s): fragments of step s, issue step s + 2 (s >= 1)
+      int n = 0;
+      if (s >= 1 && s + 2 < nsteps) n = dma_step(s + 2, ws);
+      wait_dma(n);
+      seg_barrier();
+      mfma();  // MFMA(s)
+      seg_barrier();
+      inc3(rs);
+      if (s >= 1) inc3(ws);
+      else ws = 0;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  epilogue_top2<BM, BN, 4, WN>(p, acc, q0, co0, nt, ntiles, reinterpret_cast<float*>(lds));
+}
+
+// ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, bool ARGMIN>
@@ -2535,6 +2698,17 @@ static hipError_t launch_x6w8_af32(const ConvParams& p, int batch, int phases, h
 
 static int tap_span(const ConvParams& p) { return (p.taps - 1) * (p.in_step < 0 ? -p.in_step : p.in_step); }
 
+bool bf16dm_takes(int cin, int cout, int lq, int ldx, int phases) {
+#ifdef DCX_NO_BF16DM
+  return false;
+#endif
+  ConvParams q{};
+  q.Lq = lq;
+  q.Cout = cout;
+  return cout % 256 == 0 && cin % 32 == 0 && big_tiles_pay(q, phases, 256) && 1024LL * ldx * 6 < (1LL << 31) &&
+         (long long)(cin / 16) * cout * 96 < (1LL << 31);
+}
+
 hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
   if (p.Cin % BK || p.Cout % 32 || phases < 1 || phases > kMaxPhases) return hipErrorInvalidValue;
   if (p.w6) {
@@ -2573,9 +2747,10 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
 #ifndef DCX_NO_PP
     if (p.Cout % 128 == 0 && !h && !b1) return launch_x6pp<0>(p, batch, phases, s, kname);  // x6 1-tap
 #endif
+    const bool dm_b1 = b1 && !h && p.taps == 1 && in_base_nonneg(p) && bf16dm_takes(p.Cin, p.Cout, p.Lq, p.ldx, phases);
+    if (p.x_compact && !dm_b1) return hipErrorInvalidValue;  // only conv_gemm_bf16dm reads the compact layout
 #ifndef DCX_NO_BF16DM
-    if (b1 && !h && p.taps == 1 && p.Cout % 256 == 0 && p.Cin % 32 == 0 && big_tiles_pay(p, phases, 256) &&
-        in_base_nonneg(p) && 1024LL * p.ldx * 6 < (1LL << 31) && (long long)(p.Cin / 16) * p.Cout * 96 < (1LL << 31)) {
+    if (dm_b1) {
       if (kname) *kname = "conv_gemm_bf16dm<256,256>";
       ConvParams q = p;
       q.batch = batch;
@@ -2700,6 +2875,14 @@ hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const 
 // roundings per MFMA).  By Cauchy-Schwarz sum_k |x_k e_k| <= |x| max|e|, so each approximate
 // squared distance is within 2 * kVqPrefilterBound * |x| max|e| + 8 * 2^-24 (|x|^2 + max|e|^2)
 // of the exact one; vq_rescore_kernel uses that bound.
+bool vq_bk_takes(int ncodes, int dim) {
+#ifdef DCX_NO_VQBK
+  return false;
+#endif
+  return ncodes % (256 * 16) == 0 && dim % 32 == 0 && dim / 32 >= 3 && (long long)dim * 2 * 256 < (1ll << 31) &&
+         (long long)(dim / 32) * ncodes * 128 < (1ll << 31);
+}
+
 hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipStream_t s, const char** kname) {
   constexpr int BM = 256, BN = 128;
   if (!p.w6 || !p.x6 || !p.part_val2 || p.Cin % BK || p.Cout % (BN * 16) || rows < 1) return hipErrorInvalidValue;
@@ -2707,6 +2890,14 @@ hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipSt
   q.Lq = rows;
   q.Lin = rows;
   q.taps = 1;
+  if (p.x_compact) {  // bf16 mode, compact x_pjt_in and the repacked codebook
+    if (!x_bf16 || !p.wc || !vq_bk_takes(p.Cout, p.Cin)) return hipErrorInvalidValue;
+    const int mtiles = (rows + 255) / 256, ntiles = p.Cout / 256;
+    const dim3 grid((unsigned)(((mtiles + 15) / 16) * (ntiles / 16) * 256));
+    if (kname) *kname = "vq_prefilter_bk<256,256>";
+    hipLaunchKernelGGL(vq_prefilter_bk, grid, dim3(512), 0, s, q);
+    return hipGetLastError();
+  }
   if (vq_dm_ok(p.Cout, p.Cin)) {
     const int mtiles = (rows + 255) / 256, ntiles = p.Cout / 256;
     const dim3 grid((unsigned)(((mtiles + 15) / 16) * (ntiles / 16) * 256));

@@ -59,6 +59,13 @@ struct ConvParams {
   // fp32-input (AF32) kernels: apply silu to the input while staging (the producer then writes
   // only the fp32 tensor, not its silu as well)
   int silu_in;
+  // DCX_GEMM_BF16 compact layout ([rows][C] bf16, the hi plane only; dcx_planes.h store_bf16x4):
+  // x_compact: x6 holds the input that way (conv_gemm_bf16dm and vq_prefilter_bk only);
+  // y_compact: y6 is written that way (needs round_bf16, ldy == Cout).
+  int x_compact, y_compact;
+  // bf16-mode 1x1 weights as [phase][Cin/32][Cout][32] bf16 (hi only; conv_gemm_bf16dm), or null;
+  // for the VQ prefilter: the codebook as launch_repack_codebook_bk writes it.
+  const unsigned short* wc;
 };
 
 // Independent convs issued as one launch (launch_conv_group); problem k owns logical tiles
@@ -102,6 +109,7 @@ int vq_argmin_ntiles(int ncodes);
 int vq_prefilter_ntiles(int ncodes, int dim);
 // VQ search, x6 mode: bf16x3 prefilter (approximate squared distances, per-tile top 2) ...
 // x_bf16: the rows of x are bf16 values (mid and lo planes zero), which drops the mid*hi product.
+// With x_bf16, p.x_compact and p.wc (the launch_repack_codebook_bk codebook): vq_prefilter_bk.
 hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipStream_t s, const char** kname);
 // ... then per row: certify the prefilter's winner with a rigorous error bound, or rescore every
 // candidate inside the bound in fp64.  stats (optional): [0] rows rescored, [1] codes rescored.
@@ -112,15 +120,23 @@ hipError_t launch_vq_rescore(const float* part_val, const int* part_idx, const f
 hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows, int ntiles, int32_t* codes,
                             hipStream_t s);
 hipError_t launch_row_sqnorm(const float* x, long long rows, int C, float* out, hipStream_t s);
-hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, const float* w, const float* b, long long rows,
-                          int C, float eps, int channels_first_form, hipStream_t s);
-hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, const float* dww, const float* dwb,
+// y6c: y6 in the compact bf16 layout instead of planes
+hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, int y6c, const float* w, const float* b,
+                          long long rows, int C, float eps, int channels_first_form, hipStream_t s);
+hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6c, const float* dww, const float* dwb,
                             const float* lnw, const float* lnb, int batch, int L, int C, hipStream_t s);
+// x6 codebook planes -> the per-K32 hi/mid layout of vq_prefilter_bk ((dim / 32) * ncodes * 64 bf16)
+hipError_t launch_repack_codebook_bk(const unsigned short* cb6, int ncodes, int dim, unsigned short* out,
+                                     hipStream_t s);
+// whether conv_gemm_bf16dm takes a one-tap conv of this shape (then its input may be compact)
+bool bf16dm_takes(int cin, int cout, int lq, int ldx, int phases);
+// whether vq_prefilter_bk takes the bf16-mode search (then x_pjt_in may be compact)
+bool vq_bk_takes(int ncodes, int dim);
 hipError_t launch_frame_pad(const float* audio, float* frames, unsigned short* frames6, int batch, long long n, int rows,
                             int hop, int pad_left, hipStream_t s);
 hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, long long rows, int nbins, int ld_out,
                            hipStream_t s);
-hipError_t launch_split_planes(const float* x, unsigned short* y6, long long rows, int C, hipStream_t s);
+hipError_t launch_split_planes(const float* x, unsigned short* y6, long long rows, int C, int compact, hipStream_t s);
 hipError_t launch_gather_rows(const float* table, int ntable, const int32_t* idx, long long rows, int width,
                               float* out, int32_t* n_invalid, hipStream_t s);
 hipError_t launch_conv_post_tanh(const float* x, const float* w, float bias, float* out, int batch, int L, int C,

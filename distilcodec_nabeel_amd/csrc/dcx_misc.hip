@@ -24,7 +24,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 template <int NV>
 __device__ __forceinline__ void ln_finish(f32x4 (&v)[NV], int C, float eps, int cf, const float* __restrict__ w,
                                           const float* __restrict__ b, float* __restrict__ yrow,
-                                          unsigned short* __restrict__ y6, long long row, int lane) {
+                                          unsigned short* __restrict__ y6, int y6c, long long row, int lane) {
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
@@ -50,13 +50,16 @@ __device__ __forceinline__ void ln_finish(f32x4 (&v)[NV], int C, float eps, int 
       o = (v[i] - mean) * rstd * wv + bv;
     }
     if (yrow) *reinterpret_cast<f32x4*>(yrow + c) = o;
-    if (y6) store_planes4(y6, row, C, c, o.x, o.y, o.z, o.w);
+    if (y6) {
+      if (y6c) store_bf16x4(y6, row, C, c, o.x, o.y, o.z, o.w);
+      else store_planes4(y6, row, C, c, o.x, o.y, o.z, o.w);
+    }
   }
 }
 
 template <int NV>
 __global__ void __launch_bounds__(256) ln_rows_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                       unsigned short* __restrict__ y6, const float* __restrict__ w,
+                                                       unsigned short* __restrict__ y6, int y6c, const float* __restrict__ w,
                                                        const float* __restrict__ b, long long rows, float eps, int cf) {
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -65,17 +68,17 @@ __global__ void __launch_bounds__(256) ln_rows_kernel(const float* __restrict__ 
   f32x4 v[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) v[i] = *reinterpret_cast<const f32x4*>(x + row * C + (lane + 64 * i) * 4);
-  ln_finish<NV>(v, C, eps, cf, w, b, y ? y + row * C : nullptr, y6, row, lane);
+  ln_finish<NV>(v, C, eps, cf, w, b, y ? y + row * C : nullptr, y6, y6c, row, lane);
 }
 
-hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, const float* w, const float* b, long long rows,
-                          int C, float eps, int cf, hipStream_t s) {
+hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, int y6c, const float* w, const float* b,
+                          long long rows, int C, float eps, int cf, hipStream_t s) {
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   switch (C) {
-    case 256: hipLaunchKernelGGL(ln_rows_kernel<1>, grid, block, 0, s, x, y, y6, w, b, rows, eps, cf); break;
-    case 512: hipLaunchKernelGGL(ln_rows_kernel<2>, grid, block, 0, s, x, y, y6, w, b, rows, eps, cf); break;
-    case 768: hipLaunchKernelGGL(ln_rows_kernel<3>, grid, block, 0, s, x, y, y6, w, b, rows, eps, cf); break;
-    case 1024: hipLaunchKernelGGL(ln_rows_kernel<4>, grid, block, 0, s, x, y, y6, w, b, rows, eps, cf); break;
+    case 256: hipLaunchKernelGGL(ln_rows_kernel<1>, grid, block, 0, s, x, y, y6, y6c, w, b, rows, eps, cf); break;
+    case 512: hipLaunchKernelGGL(ln_rows_kernel<2>, grid, block, 0, s, x, y, y6, y6c, w, b, rows, eps, cf); break;
+    case 768: hipLaunchKernelGGL(ln_rows_kernel<3>, grid, block, 0, s, x, y, y6, y6c, w, b, rows, eps, cf); break;
+    case 1024: hipLaunchKernelGGL(ln_rows_kernel<4>, grid, block, 0, s, x, y, y6, y6c, w, b, rows, eps, cf); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -85,7 +88,7 @@ hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, const fl
 // F.layer_norm over channels.  dww is packed [7][C].  One wave per output row.
 template <int NV>
 __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                         unsigned short* __restrict__ y6,
+                                                         unsigned short* __restrict__ y6, int y6c,
                                                          const float* __restrict__ dww, const float* __restrict__ dwb,
                                                          const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                          int L, long long rows) {
@@ -118,18 +121,18 @@ __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict_
     }
     v[i] = acc + *reinterpret_cast<const f32x4*>(dwb + c);
   }
-  ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y ? y + row * C : nullptr, y6, row, lane);
+  ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y ? y + row * C : nullptr, y6, y6c, row, lane);
 }
 
-hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, const float* dww, const float* dwb,
+hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6c, const float* dww, const float* dwb,
                             const float* lnw, const float* lnb, int batch, int L, int C, hipStream_t s) {
   const long long rows = (long long)batch * L;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   switch (C) {
-    case 256: hipLaunchKernelGGL(dwconv_ln_kernel<1>, grid, block, 0, s, x, y, y6, dww, dwb, lnw, lnb, L, rows); break;
-    case 512: hipLaunchKernelGGL(dwconv_ln_kernel<2>, grid, block, 0, s, x, y, y6, dww, dwb, lnw, lnb, L, rows); break;
-    case 768: hipLaunchKernelGGL(dwconv_ln_kernel<3>, grid, block, 0, s, x, y, y6, dww, dwb, lnw, lnb, L, rows); break;
-    case 1024: hipLaunchKernelGGL(dwconv_ln_kernel<4>, grid, block, 0, s, x, y, y6, dww, dwb, lnw, lnb, L, rows); break;
+    case 256: hipLaunchKernelGGL(dwconv_ln_kernel<1>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, rows); break;
+    case 512: hipLaunchKernelGGL(dwconv_ln_kernel<2>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, rows); break;
+    case 768: hipLaunchKernelGGL(dwconv_ln_kernel<3>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, rows); break;
+    case 1024: hipLaunchKernelGGL(dwconv_ln_kernel<4>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, rows); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -204,24 +207,26 @@ hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, 
   return hipGetLastError();
 }
 
-// fp32 [rows][C] -> planes (boundary conversion for tensors handed in by the caller).
+// fp32 [rows][C] -> planes, or (compact) bf16 [rows][C] (boundary conversion for tensors handed in
+// by the caller).
 __global__ void __launch_bounds__(256) split_planes_kernel(const float* __restrict__ x, unsigned short* __restrict__ y6,
-                                                            long long rows, int C) {
+                                                            long long rows, int C, int compact) {
   const long long total4 = rows * C / 4;
   for (long long i4 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i4 < total4;
        i4 += (long long)gridDim.x * blockDim.x) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(x + i4 * 4);
     const long long i = i4 * 4;
-    store_planes4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
+    if (compact) store_bf16x4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
+    else store_planes4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
   }
 }
 
-hipError_t launch_split_planes(const float* x, unsigned short* y6, long long rows, int C, hipStream_t s) {
+hipError_t launch_split_planes(const float* x, unsigned short* y6, long long rows, int C, int compact, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
   const long long total4 = rows * C / 4;
   unsigned g = (unsigned)((total4 + 255) / 256);
   if (g > 8192) g = 8192;
-  hipLaunchKernelGGL(split_planes_kernel, dim3(g), dim3(256), 0, s, x, y6, rows, C);
+  hipLaunchKernelGGL(split_planes_kernel, dim3(g), dim3(256), 0, s, x, y6, rows, C, compact);
   return hipGetLastError();
 }
 
@@ -561,6 +566,33 @@ hipError_t launch_resample_poly(const float* x, int batch, long long n_in, long 
                                 hipStream_t s) {
   const dim3 grid((unsigned)((n_out + 255) / 256), (unsigned)batch);
   hipLaunchKernelGGL(resample_poly_kernel, grid, dim3(256), 0, s, x, n_in, xs, h, hlen, up, down, pre, y, n_out, ys);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Codebook for the bf16-mode VQ prefilter (vq_prefilter_bk): the hi and mid planes of the x6
+// codebook ([CD/16][NC][2 halves][3 planes][8], ConvParams::w6 layout) repacked per K32 step as
+// [CD/32][NC][8 pieces][8] bf16, piece = (chunk half cc, channel half hh, plane hi/mid) =
+// (cc * 2 + hh) * 2 + pl: 128 contiguous bytes per code per step.  One thread per 16-byte piece.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) repack_codebook_bk_kernel(const unsigned short* __restrict__ cb6, int ncodes,
+                                                                 long long pieces, unsigned short* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= pieces) return;
+  const int pc = (int)(i & 7);
+  const long long sn = i >> 3;  // step * ncodes + code
+  const long long st = sn / ncodes, n = sn - st * ncodes;
+  const int cc = pc >> 2, hh = (pc >> 1) & 1, pl = pc & 1;
+  const unsigned short* src = cb6 + ((2 * st + cc) * ncodes + n) * 48 + hh * 24 + pl * 8;
+  *reinterpret_cast<uint4*>(out + i * 8) = *reinterpret_cast<const uint4*>(src);
+}
+
+hipError_t launch_repack_codebook_bk(const unsigned short* cb6, int ncodes, int dim, unsigned short* out,
+                                     hipStream_t s) {
+  if (dim % 32) return hipErrorInvalidValue;
+  const long long pieces = (long long)(dim / 32) * ncodes * 8;
+  hipLaunchKernelGGL(repack_codebook_bk_kernel, dim3((unsigned)((pieces + 255) / 256)), dim3(256), 0, s, cb6, ncodes,
+                     pieces, out);
   return hipGetLastError();
 }
 

@@ -56,4 +56,16 @@ __device__ __forceinline__ void store_planes4(unsigned short* base, long long ro
   *reinterpret_cast<s16x4p*>(dst + 16) = lv;
 }
 
+// Compact bf16 layout (DCX_GEMM_BF16 mode, tensors whose consumers read only the hi plane):
+// [rows][C] bf16 = hi only, 2 bytes per element.  Store 4 consecutive channels c..c+3 (c % 4 == 0).
+__device__ __forceinline__ void store_bf16x4(unsigned short* base, long long row, int C, int c, float a, float b,
+                                             float cc, float d) {
+  s16x4p hv;
+  hv[0] = (short)bf16_bits(a);
+  hv[1] = (short)bf16_bits(b);
+  hv[2] = (short)bf16_bits(cc);
+  hv[3] = (short)bf16_bits(d);
+  *reinterpret_cast<s16x4p*>(base + row * (long long)C + c) = hv;
+}
+
 }  // namespace dcx

@@ -92,3 +92,35 @@ def test_codec_flag_switches_and_restores(codec, golden):
     r32, _, _ = codec.encode([[a, 24000]], raw_audio=True, codes_only=True)
     assert (r32.codes.cpu().numpy()[0, :, :, 0] == g["codes"]).mean() >= 0.97
     assert (r16.codes == r32.codes).double().mean() >= 0.90
+
+
+@pytest.mark.parametrize("B,secs", [(2, 3), (4, 11)])
+def test_compact_layout_same_bits(beng, cfg, state, B, secs):
+    """bf16 mode stores the activations read by conv_gemm_bf16dm and vq_prefilter_bk in the compact
+    layout (hi plane only, 2 B per element).  The GEMMs read the same hi values either way, so the
+    encoder features and x_pjt_in equal the planes-layout run (DCX_NO_COMPACT=1) bit for bit, and the
+    codes too (both exact argmins).  4 x 11 s puts every 1x1 conv on conv_gemm_bf16dm; 2 x 3 s mixes
+    compact and planes consumers (the narrow 4C -> C convs fall back to planes kernels)."""
+    import os
+
+    from distilcodec_nabeel_amd import synth
+    from distilcodec_nabeel_amd.engine import NativeCodec
+
+    os.environ["DCX_NO_COMPACT"] = "1"
+    try:
+        plain = NativeCodec(cfg, {"encoder": state["encoder"], "quantizer": state["quantizer"]}, "cuda:0",
+                            with_generator=False, gemm="bf16")
+    finally:
+        del os.environ["DCX_NO_COMPACT"]
+    n = 24000 * secs
+    audio = torch.zeros(B, n + 1)
+    for i, c in enumerate(synth.clips(B, n, seed=11, kind="mix")):
+        audio[i, 1:] = torch.from_numpy(c)
+    audio = audio.cuda()
+    outs = []
+    for eng in (beng, plain):
+        feat = eng.encode(eng.mel(audio))
+        codes, pin, _, q = eng.vq_encode(feat, want_fup=False)
+        outs.append((feat, codes, pin, q))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
