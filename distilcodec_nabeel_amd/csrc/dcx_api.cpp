@@ -527,7 +527,7 @@ struct ConvCall {
   float* y2 = nullptr;           // silu(v), fp32
   unsigned short* y6 = nullptr;  // planes of v
   unsigned short* y6s = nullptr; // planes of silu(v)
-  bool y6c = false;              // y6 in the compact bf16 layout
+  int y6c = 0;                   // y6 layout (ConvParams::y_compact): 0 planes, 1 compact bf16, 2 hm
   float* macc = nullptr;
   const float* res = nullptr;
   const float* gamma = nullptr;
@@ -535,7 +535,7 @@ struct ConvCall {
   bool exact = false;  // keep x6 arithmetic in bf16 mode (the reference's fp32 mel front end)
   bool silu_in = false;  // fp32 input: the conv consumes silu(x) (applied while staging)
   void silu_to(const Act& a) { y2 = a.f; y6s = a.p; }
-  void out_to(const Act& a) { y = a.f; y6 = a.p; y6c = a.c1; }
+  void out_to(const Act& a) { y = a.f; y6 = a.p; y6c = a.c1 ? 1 : 0; }
 };
 
 // Planes-mode convs with Cout <= 64, Cin <= 128 and a tap halo take an fp32 input (split while
@@ -580,10 +580,12 @@ int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32,
   p.nprod = one ? 1 : 6;
   p.round_bf16 = one;
   p.silu_in = c.silu_in;
-  p.x_compact = x6 && c.x.p && c.x.c1;
-  p.y_compact = c.y6 && c.y6c;
+  p.x_compact = x6 && c.x.p && c.x.c1 ? 1 : 0;
+  p.y_compact = c.y6 ? c.y6c : 0;
   p.wc = one && h->compact ? w.wc : nullptr;
-  if ((p.x_compact || p.y_compact) && !one) return fail(h, DCX_ERR_STATE, "internal: compact layout outside bf16 mode");
+  if ((p.x_compact == 1 || p.y_compact == 1) && !one)
+    return fail(h, DCX_ERR_STATE, "internal: compact layout outside bf16 mode");
+  if (p.y_compact == 2 && (!x6 || one)) return fail(h, DCX_ERR_STATE, "internal: hm layout outside x6 mode");
   return DCX_OK;
 }
 
@@ -696,7 +698,7 @@ int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, in
   ConvCall c2 = pointwise(hid, M);
   c2.y = x;
   c2.y6 = out6;
-  c2.y6c = out6 && out6c;
+  c2.y6c = out6 && out6c ? 1 : 0;
   c2.res = x;
   c2.gamma = bw.gamma;
   c2.epi = dcx::EPI_GAMMA_RES;
@@ -795,11 +797,13 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   const bool x6c = X6 && takes_compact(h, h->vq_pin, M);
   // bf16 mode: x_pjt_in compact for vq_prefilter_bk (the repacked codebook exists iff it takes the shape)
   const bool p6c = P6 && h->compact && h->gemm_mode == DCX_GEMM_BF16 && h->codebook_bk;
+  // x6 mode: x_pjt_in in the "hm" layout (hi and mid per 32 channels) for vq_prefilter_dm
+  const bool p6hm = P6 && h->compact && h->gemm_mode == DCX_GEMM_X6 && h->codebook_bk && dcx::vq_hm_takes(NC, CD);
   RUN(run_block(h, h->vq_down_blk, X, X6, B, T, ln, hid, s, x6c));
   ConvCall cp = pointwise(CAct(X, X6, x6c), M);
   cp.y = P;
   cp.y6 = P6;
-  cp.y6c = p6c;
+  cp.y6c = p6c ? 1 : p6hm ? 2 : 0;
   RUN(run_conv(h, h->vq_pin, cp, s));
   LAUNCH(h, s, "row_sqnorm", 2.0 * M * CD, 4.0 * M * CD, dcx::launch_row_sqnorm(P, M, CD, x2, s));
   {
@@ -807,8 +811,8 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
     p.x = P; p.x6 = P6; p.w = h->codebook; p.w6 = x6 ? h->codebook6 : nullptr;
     p.Cin = CD; p.Cout = NC; p.ldx = CD; p.taps = 1; p.in_step = 1; p.out_mul = 1;
     p.x2 = x2; p.e2 = h->e2; p.part_val = pv; p.part_idx = pi; p.part_val2 = pv2;
-    p.x_compact = p6c;
-    p.wc = p6c ? h->codebook_bk : nullptr;
+    p.x_compact = p6c ? 1 : p6hm ? 2 : 0;
+    p.wc = p6c || p6hm ? h->codebook_bk : nullptr;
     ProfScope ps(h, s);
     const char* kname = "vq";
     if (x6) {

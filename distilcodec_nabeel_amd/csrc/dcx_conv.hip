@@ -168,7 +168,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
   const int wm = wave / WN, wn = wave % WN;
   const int lrow = lane & 31, rhalf = 4 * (lane >> 5);
   const long long ob = (long long)b * p.y_bstride;
-  unsigned short* y6 = p.y6 ? p.y6 + ob * (p.y_compact ? 1 : 3) : nullptr;
+  unsigned short* y6 = p.y6 ? p.y6 + ob * (p.y_compact == 1 ? 1 : p.y_compact == 2 ? 2 : 3) : nullptr;
   unsigned short* y6s = p.y6s ? p.y6s + ob * 3 : nullptr;
   static_assert(NT % (BN / 4) == 0, "each thread keeps one 4-channel group");
   const int c4 = (tid % (BN / 4)) * 4, trow = tid / (BN / 4), co = co0 + c4;
@@ -266,7 +266,8 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
       }
       if (p.y) *reinterpret_cast<f32x4*>(p.y + o) = x;
       if (y6) {
-        if (p.y_compact) store_bf16x4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
+        if (p.y_compact == 1) store_bf16x4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
+        else if (p.y_compact == 2) store_hm4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
         else store_planes4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
       }
       if (p.y2 || y6s) {
@@ -1996,7 +1997,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
   const int nsteps = p.Cin / 32;
   // input: planes (hi pieces at 48-byte strides, 6 bytes per element) or compact bf16 (x_compact:
   // one contiguous 64-byte run per row and step); weights: planes w6 or compact wc likewise
-  const int xc = p.x_compact ? 1 : 3;
+  const int xc = p.x_compact == 1 ? 1 : 3;
   const int arow = p.ldx * 2 * xc, a_kq = 16 * xc, a_step = 64 * xc;
   const int row0 = q0 + p.in_base[ph];  // >= 0 for 1x1 convs; the descriptor covers the tile's rows
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
@@ -2373,27 +2374,40 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_dm(const ConvParams p) {
   if (mt >= mtiles) return;  // whole workgroup, before any barrier
   const int q0 = mt * BM, co0 = nt * BN;
   const int nsteps = p.Cin / BK;
-  const int arow = p.ldx * 6;  // bytes per planes row
+  // hm (p.x_compact == 2, x6 mode): x_pjt_in in the "hm" layout and the codebook as
+  // launch_repack_codebook_bk packs it (p.wc), so each row's / code's four pieces of a K16 step are
+  // one contiguous 64-byte run; otherwise planes (two 32-byte runs per 96-byte chunk)
+  const bool hm = p.x_compact == 2;
+  const int arow = p.ldx * (hm ? 4 : 6);  // bytes per input row
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.x6 + (long long)q0 * p.ldx * 3), 0, min(BM, p.Lq - q0) * arow, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.w6, 0, nsteps * p.Cout * 96, 0x00020000);
+      (void*)(p.x6 + (long long)q0 * p.ldx * (hm ? 2 : 3)), 0, min(BM, p.Lq - q0) * arow, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      hm ? __builtin_amdgcn_make_buffer_rsrc((void*)p.wc, 0, nsteps * p.Cout * 64, 0x00020000)
+         : __builtin_amdgcn_make_buffer_rsrc((void*)p.w6, 0, nsteps * p.Cout * 96, 0x00020000);
 
   int a_off[PW], b_off[PW];
 #pragma unroll
   for (int i = 0; i < PW; ++i) {
     const int u = (group * G_I + i * 4 + gw) * 64 + lane;
     const int row = u >> 2, pc = (u & 3) ^ ((row >> 2) & 3);
-    const int poff = (pc >> 1) * 48 + (pc & 1) * 16;  // (half, plane) within a 96-byte K16 chunk
+    // (half, plane) within a 96-byte K16 chunk, or within the 64-byte hm run
+    const int poff = hm ? ((pc >> 1) * 2 + (pc & 1)) * 16 : (pc >> 1) * 48 + (pc & 1) * 16;
     a_off[i] = row * arow + poff;
-    b_off[i] = (co0 + row) * 96 + poff;
+    b_off[i] = (co0 + row) * (hm ? 128 : 96) + poff;
   }
+  // step c's byte offset: planes c * 96 (input) / c * Cout * 96 (codebook); hm: K32 step c >> 1,
+  // half (c & 1) of its 128-byte run
+  const int a_step = hm ? 128 : 96;
+  const int b_step = hm ? p.Cout * 128 : p.Cout * 96;
   unsigned short* const a_dst = lds + (group * G_I + gw) * 512;
   unsigned short* const b_dst = lds + 3 * ABUF + (group * G_I + gw) * 512;
   auto dma_step = [&](int c, int slot) {
+    const int ao = hm ? (c >> 1) * a_step + (c & 1) * 64 : c * a_step;
+    const int bo = hm ? (c >> 1) * b_step + (c & 1) * 64 : c * b_step;
 #pragma unroll
-    for (int i = 0; i < PW; ++i) dma16(rx, a_dst + slot * ABUF + i * 2048, a_off[i] + c * 96, 0);
+    for (int i = 0; i < PW; ++i) dma16(rx, a_dst + slot * ABUF + i * 2048, a_off[i] + ao, 0);
 #pragma unroll
-    for (int i = 0; i < PW; ++i) dma16(rw, b_dst + slot * BBUF + i * 2048, b_off[i], c * p.Cout * 96);
+    for (int i = 0; i < PW; ++i) dma16(rw, b_dst + slot * BBUF + i * 2048, b_off[i], bo);
     return 2 * PW;
   };
 
@@ -2748,7 +2762,7 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
     if (p.Cout % 128 == 0 && !h && !b1) return launch_x6pp<0>(p, batch, phases, s, kname);  // x6 1-tap
 #endif
     const bool dm_b1 = b1 && !h && p.taps == 1 && in_base_nonneg(p) && bf16dm_takes(p.Cin, p.Cout, p.Lq, p.ldx, phases);
-    if (p.x_compact && !dm_b1) return hipErrorInvalidValue;  // only conv_gemm_bf16dm reads the compact layout
+    if (p.x_compact && (!dm_b1 || p.x_compact != 1)) return hipErrorInvalidValue;  // only conv_gemm_bf16dm reads it
 #ifndef DCX_NO_BF16DM
     if (dm_b1) {
       if (kname) *kname = "conv_gemm_bf16dm<256,256>";
@@ -2883,6 +2897,8 @@ bool vq_bk_takes(int ncodes, int dim) {
          (long long)(dim / 32) * ncodes * 128 < (1ll << 31);
 }
 
+bool vq_hm_takes(int ncodes, int dim) { return vq_bk_takes(ncodes, dim) && vq_dm_ok(ncodes, dim); }
+
 hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipStream_t s, const char** kname) {
   constexpr int BM = 256, BN = 128;
   if (!p.w6 || !p.x6 || !p.part_val2 || p.Cin % BK || p.Cout % (BN * 16) || rows < 1) return hipErrorInvalidValue;
@@ -2890,7 +2906,15 @@ hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipSt
   q.Lq = rows;
   q.Lin = rows;
   q.taps = 1;
-  if (p.x_compact) {  // bf16 mode, compact x_pjt_in and the repacked codebook
+  if (p.x_compact == 2) {  // x6 mode, "hm" x_pjt_in and the repacked codebook: vq_prefilter_dm
+    if (x_bf16 || !p.wc || !vq_hm_takes(p.Cout, p.Cin)) return hipErrorInvalidValue;
+    const int mtiles = (rows + 255) / 256, ntiles = p.Cout / 256;
+    const dim3 grid((unsigned)(((mtiles + 15) / 16) * (ntiles / 16) * 256));
+    if (kname) *kname = "vq_prefilter_dm<256,256>";
+    hipLaunchKernelGGL((vq_prefilter_dm<true>), grid, dim3(512), 0, s, q);
+    return hipGetLastError();
+  }
+  if (p.x_compact == 1) {  // bf16 mode, compact x_pjt_in and the repacked codebook
     if (!x_bf16 || !p.wc || !vq_bk_takes(p.Cout, p.Cin)) return hipErrorInvalidValue;
     const int mtiles = (rows + 255) / 256, ntiles = p.Cout / 256;
     const dim3 grid((unsigned)(((mtiles + 15) / 16) * (ntiles / 16) * 256));

@@ -59,9 +59,11 @@ struct ConvParams {
   // fp32-input (AF32) kernels: apply silu to the input while staging (the producer then writes
   // only the fp32 tensor, not its silu as well)
   int silu_in;
-  // DCX_GEMM_BF16 compact layout ([rows][C] bf16, the hi plane only; dcx_planes.h store_bf16x4):
-  // x_compact: x6 holds the input that way (conv_gemm_bf16dm and vq_prefilter_bk only);
-  // y_compact: y6 is written that way (needs round_bf16, ldy == Cout).
+  // Layouts other than planes for x6 / y6 (dcx_planes.h), 0 = planes:
+  //   1 = compact bf16 ([rows][C], hi plane only; bf16 mode; read by conv_gemm_bf16dm and
+  //       vq_prefilter_bk; written with round_bf16, ldy == Cout);
+  //   2 = "hm" ([rows][C/32][8][8], hi and mid planes per 32 channels; x6-mode x_pjt_in, read by
+  //       vq_prefilter_dm only).
   int x_compact, y_compact;
   // bf16-mode 1x1 weights as [phase][Cin/32][Cout][32] bf16 (hi only; conv_gemm_bf16dm), or null;
   // for the VQ prefilter: the codebook as launch_repack_codebook_bk writes it.
@@ -109,7 +111,8 @@ int vq_argmin_ntiles(int ncodes);
 int vq_prefilter_ntiles(int ncodes, int dim);
 // VQ search, x6 mode: bf16x3 prefilter (approximate squared distances, per-tile top 2) ...
 // x_bf16: the rows of x are bf16 values (mid and lo planes zero), which drops the mid*hi product.
-// With x_bf16, p.x_compact and p.wc (the launch_repack_codebook_bk codebook): vq_prefilter_bk.
+// p.x_compact == 1 (bf16 mode) / 2 (x6 mode, "hm" layout) with p.wc the launch_repack_codebook_bk
+// codebook: vq_prefilter_bk / vq_prefilter_dm reading contiguous runs.
 hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipStream_t s, const char** kname);
 // ... then per row: certify the prefilter's winner with a rigorous error bound, or rescore every
 // candidate inside the bound in fp64.  stats (optional): [0] rows rescored, [1] codes rescored.
@@ -132,6 +135,8 @@ hipError_t launch_repack_codebook_bk(const unsigned short* cb6, int ncodes, int 
 bool bf16dm_takes(int cin, int cout, int lq, int ldx, int phases);
 // whether vq_prefilter_bk takes the bf16-mode search (then x_pjt_in may be compact)
 bool vq_bk_takes(int ncodes, int dim);
+// whether vq_prefilter_dm takes the x6-mode search with x_pjt_in in the "hm" layout
+bool vq_hm_takes(int ncodes, int dim);
 hipError_t launch_frame_pad(const float* audio, float* frames, unsigned short* frames6, int batch, long long n, int rows,
                             int hop, int pad_left, hipStream_t s);
 hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, long long rows, int nbins, int ld_out,

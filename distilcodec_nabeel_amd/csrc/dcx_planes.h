@@ -68,4 +68,23 @@ __device__ __forceinline__ void store_bf16x4(unsigned short* base, long long row
   *reinterpret_cast<s16x4p*>(base + row * (long long)C + c) = hv;
 }
 
+// "hm" layout (x6-mode x_pjt_in, read only by vq_prefilter_dm): the hi and mid planes per 32
+// channels as [rows][C/32][8 pieces][8] bf16, piece = ((c >> 3) & 3) * 2 + plane (4 B per element),
+// the per-K32 layout of launch_repack_codebook_bk.  Store 4 consecutive channels c..c+3 (c % 4 == 0).
+__device__ __forceinline__ void store_hm4(unsigned short* base, long long row, int C, int c, float a, float b,
+                                          float cc, float d) {
+  s16x4p hv, mv;
+  const float v[4] = {a, b, cc, d};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    unsigned short h, m, l;
+    split3(v[e], h, m, l);
+    hv[e] = (short)h;
+    mv[e] = (short)m;
+  }
+  unsigned short* dst = base + row * (long long)C * 2 + (c >> 5) * 64 + ((c >> 3) & 3) * 16 + (c & 7);
+  *reinterpret_cast<s16x4p*>(dst) = hv;
+  *reinterpret_cast<s16x4p*>(dst + 8) = mv;
+}
+
 }  // namespace dcx

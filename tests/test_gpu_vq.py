@@ -111,3 +111,26 @@ def test_workspace_without_generator(veng):
     ws = int(veng.L.dcx_workspace_size(veng.h, 32, 937))
     gen = (5 * 4 + 8 * 6) * 32 * 937 * 8192
     assert 0 < ws < gen // 3
+
+
+def test_hm_layout_same_codes(veng, cfg, state):
+    """x6 mode hands x_pjt_in to vq_prefilter_dm in the "hm" layout (hi and mid planes per 32
+    channels) with the codebook repacked the same way; DCX_NO_COMPACT=1 keeps the planes layout.
+    Both searches are exact, so x_pjt_in and the codes agree bit for bit."""
+    import os
+
+    from distilcodec_nabeel_amd.engine import NativeCodec
+
+    os.environ["DCX_NO_COMPACT"] = "1"
+    try:
+        plain = NativeCodec(cfg, {"encoder": state["encoder"], "quantizer": state["quantizer"]}, "cuda:0",
+                            with_generator=False, gemm="x6")
+    finally:
+        del os.environ["DCX_NO_COMPACT"]
+    g = torch.Generator().manual_seed(3)
+    feat = (torch.randn(3, 700, 1024, generator=g) * 0.7).cuda()
+    a = veng.vq_encode(feat, want_fup=False, want_quantized=False)
+    b = plain.vq_encode(feat, want_fup=False, want_quantized=False)
+    assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
+    np.testing.assert_array_equal(a[0].cpu().numpy().reshape(-1), _argmin_fp64(a[1].reshape(-1, a[1].shape[-1]),
+                                                                                 torch.from_numpy(state["quantizer"][KEY][0])))
