@@ -125,56 +125,59 @@ class NativeCodec:
         return int(self.L.dcx_num_frames(self.h, n_samples))
 
     # ------------------------------------------------------------------ stages
-    def mel(self, audio: torch.Tensor) -> torch.Tensor:
+    # Every stage takes an optional caller-owned workspace `ws` (see `workspace`): a captured hipGraph
+    # must keep the buffer it was recorded with.
+    def mel(self, audio: torch.Tensor, ws: torch.Tensor | None = None) -> torch.Tensor:
         """audio (B, N) fp32 (with the reference's leading zero) -> mel (B, T, n_mels)."""
         audio = self._dev(audio, torch.float32)
         B, N = audio.shape
         T = self.num_frames(N)
         out = torch.empty(B, T, self.n_mels, device=self.device)
-        ws = self.workspace(B, T)
+        ws = self.workspace(B, T, ws)
         with torch.cuda.device(self.device):
             self._check(self.L.dcx_mel(self.h, self._ptr(audio), B, N, self._ptr(out), self._ptr(ws), ws.numel(), self._stream()))
         return out
 
-    def encode(self, mel: torch.Tensor) -> torch.Tensor:
+    def encode(self, mel: torch.Tensor, ws: torch.Tensor | None = None) -> torch.Tensor:
         mel = self._dev(mel, torch.float32)
         B, T, _ = mel.shape
         out = torch.empty(B, T, self.cfg["encoder"]["dims"][-1], device=self.device)
-        ws = self.workspace(B, T)
+        ws = self.workspace(B, T, ws)
         with torch.cuda.device(self.device):
             self._check(self.L.dcx_encode(self.h, self._ptr(mel), B, T, self._ptr(out), self._ptr(ws), ws.numel(), self._stream()))
         return out
 
-    def vq_encode(self, feat: torch.Tensor, want_pjt_in=True, want_fup=True, want_quantized=True):
+    def vq_encode(self, feat: torch.Tensor, want_pjt_in=True, want_fup=True, want_quantized=True,
+                  ws: torch.Tensor | None = None):
         feat = self._dev(feat, torch.float32)
         B, T, _ = feat.shape
         codes = torch.empty(B, T, dtype=torch.int32, device=self.device)
         pin = torch.empty(B, T, self.CD, device=self.device) if want_pjt_in else None
         fup = torch.empty(B, T, self.CD, device=self.device) if want_fup else None
         q = torch.empty(B, T, self.D, device=self.device) if want_quantized else None
-        ws = self.workspace(B, T)
+        ws = self.workspace(B, T, ws)
         with torch.cuda.device(self.device):
             self._check(self.L.dcx_vq_encode(self.h, self._ptr(feat), B, T, self._ptr(codes), self._ptr(pin), self._ptr(fup),
                                              self._ptr(q), self._ptr(ws), ws.numel(), self._stream()))
         return codes, pin, fup, q
 
-    def vq_decode(self, codes: torch.Tensor) -> torch.Tensor:
+    def vq_decode(self, codes: torch.Tensor, ws: torch.Tensor | None = None) -> torch.Tensor:
         codes = self._dev(codes, torch.int32)
         B, T = codes.shape
         z = torch.empty(B, T, self.D, device=self.device)
-        ws = self.workspace(B, T)
+        ws = self.workspace(B, T, ws)
         with torch.cuda.device(self.device):
             self._check(self.L.dcx_vq_decode(self.h, self._ptr(codes), B, T, self._ptr(z), None, self._ptr(ws), ws.numel(),
                                              self._stream()))
         return z
 
-    def generate(self, z: torch.Tensor) -> torch.Tensor:
+    def generate(self, z: torch.Tensor, ws: torch.Tensor | None = None) -> torch.Tensor:
         if not self.with_generator:
             raise RuntimeError("this engine was built without generator weights")
         z = self._dev(z, torch.float32)
         B, T, _ = z.shape
         wav = torch.empty(B, self.hop * T, device=self.device)
-        ws = self.workspace(B, T)
+        ws = self.workspace(B, T, ws)
         with torch.cuda.device(self.device):
             self._check(self.L.dcx_generate(self.h, self._ptr(z), B, T, self._ptr(wav), self._ptr(ws), ws.numel(), self._stream()))
         return wav

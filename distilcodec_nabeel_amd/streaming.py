@@ -99,10 +99,18 @@ class HaloStream:
     frame sees the same inputs as in a full-clip run.  Latency: about enc_halo + gen_halo + 3
     frames of look-ahead.  Results equal the full clip up to fp32 summation order (window lengths
     pick other conv tilings).
+
+    Fixed windows (`push_samples`): every push of at most `push_samples` samples runs on windows of
+    one shape, the encoder window zero-padded past the received audio and the generator window
+    padded with code 0 past the last code.  The padding only reaches frames that are not final
+    yet (it sits beyond the receptive field of every emitted frame), so the output is the same
+    function of the input.  `graph=True` captures the two window steps (mel -> encoder -> VQ
+    search; VQ decode -> generator) in two HIP graphs and replays them, bit-equal to the eager
+    fixed-window run; `flush` runs the variable-shape eager step (the clip end is reflected).
     """
 
     def __init__(self, engine: NativeCodec, enc_halo: int | None = None, gen_halo: int | None = None,
-                 record_codes: bool = False):
+                 record_codes: bool = False, push_samples: int | None = None, graph: bool = False):
         self.engine = engine
         self.code_log = [] if record_codes else None  # every final code, in order (tests / token output)
         e, d = receptive_field(engine.cfg)
@@ -118,7 +126,85 @@ class HaloStream:
         self.c_off = 0
         self.emitted = 0  # frames whose audio was returned
         self.done = False
+        self.push_samples = push_samples
+        self.graphs = None
+        if graph and not push_samples:
+            raise ValueError("graph=True needs fixed windows: pass push_samples")
+        if push_samples:
+            self._init_windows(push_samples, graph)
 
+    # ------------------------------------------------------------------ fixed windows
+    def _init_windows(self, push: int, graph: bool):
+        eng, hop = self.engine, self.hop
+        # encoder window: received audio from frame a = (codes done) - enc_halo - 2; with codes done
+        # = (mel frames of the previous audio) - enc_halo, it spans at most push + 639 + hop (2 e + 2)
+        # samples (the first pushes, a = 0, span less)
+        self.n_enc = push + 640 + hop * (2 * self.enc_halo + 2)
+        # generator window: the frames that became final (at most ceil(push / hop) + 1) and gen_halo
+        # on each side
+        self.t_gen = -(-push // hop) + 1 + 2 * self.gen_halo
+        dev = eng.device
+        self.a_win = torch.zeros(1, self.n_enc, device=dev)
+        self.c_win = torch.zeros(1, self.t_gen, dtype=torch.int32, device=dev)
+        t_enc = eng.num_frames(self.n_enc)
+        self.ws = torch.empty(max(eng.workspace_size(1, t_enc), eng.workspace_size(1, self.t_gen)),
+                              dtype=torch.uint8, device=dev)
+        self.codes_win = self.wav_win = None
+        if graph:
+            with torch.cuda.device(dev):
+                s = torch.cuda.Stream(dev)  # eager warm-up (first-launch work) off the capture
+                s.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(s):
+                    self._enc_body()
+                    self._gen_body()
+                torch.cuda.current_stream(dev).wait_stream(s)
+                g_enc, g_gen = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g_enc):
+                    self.codes_win = self._enc_body()
+                with torch.cuda.graph(g_gen):
+                    self.wav_win = self._gen_body()
+            self.graphs = (g_enc, g_gen)
+
+    def _enc_body(self):
+        eng = self.engine
+        feat = eng.encode(eng.mel(self.a_win, ws=self.ws), ws=self.ws)
+        return eng.vq_encode(feat, want_pjt_in=False, want_fup=False, want_quantized=False, ws=self.ws)[0]
+
+    def _gen_body(self):
+        eng = self.engine
+        return eng.generate(eng.vq_decode(self.c_win, ws=self.ws), ws=self.ws)
+
+    def _encode_window(self, seg: torch.Tensor, final: bool) -> torch.Tensor:
+        """Codes of the window whose audio is seg (from its first sample on)."""
+        eng = self.engine
+        if self.push_samples is None or final:
+            return eng.vq_encode(eng.encode(eng.mel(seg.unsqueeze(0))), want_pjt_in=False, want_fup=False,
+                                 want_quantized=False)[0][0]
+        n = seg.numel()
+        if n > self.n_enc:
+            raise ValueError(f"push larger than the fixed window allows (push_samples={self.push_samples})")
+        self.a_win[0, :n].copy_(seg)
+        self.a_win[0, n:].zero_()
+        if self.graphs:
+            self.graphs[0].replay()
+            return self.codes_win[0]
+        return self._enc_body()[0]
+
+    def _generate_window(self, codes: torch.Tensor, final: bool) -> torch.Tensor:
+        eng = self.engine
+        if self.push_samples is None or final:
+            return eng.generate(eng.vq_decode(codes.unsqueeze(0)))[0]
+        n = codes.numel()
+        if n > self.t_gen:
+            raise ValueError(f"push larger than the fixed window allows (push_samples={self.push_samples})")
+        self.c_win[0, :n].copy_(codes)
+        self.c_win[0, n:].zero_()
+        if self.graphs:
+            self.graphs[1].replay()
+            return self.wav_win[0]
+        return self._gen_body()[0]
+
+    # ------------------------------------------------------------------ stream
     @property
     def n_codes(self) -> int:
         return self.c_off + self.codes.numel()
@@ -135,10 +221,9 @@ class HaloStream:
         c_done, c_new = self.n_codes, self._final_codes(final)
         if c_new > c_done:
             a = max(0, c_done - self.enc_halo - 2)
-            seg = self.audio[256 * a - self.a_off:].unsqueeze(0)
-            feat = eng.encode(eng.mel(seg))
-            codes = eng.vq_encode(feat, want_pjt_in=False, want_fup=False, want_quantized=False)[0][0]
-            new_codes = codes[c_done - a:c_new - a]
+            seg = self.audio[256 * a - self.a_off:]
+            codes = self._encode_window(seg, final)
+            new_codes = codes[c_done - a:c_new - a].clone()
             self.codes = torch.cat([self.codes, new_codes])
             if self.code_log is not None:
                 self.code_log.append(new_codes)
@@ -150,8 +235,8 @@ class HaloStream:
         if f_new <= self.emitted:
             return torch.empty(0, device=eng.device)
         g0, g1 = max(0, self.emitted - self.gen_halo), min(T, f_new + self.gen_halo)
-        wav = eng.generate(eng.vq_decode(self.codes[g0 - self.c_off:g1 - self.c_off].unsqueeze(0)))[0]
-        out = wav[self.hop * (self.emitted - g0):self.hop * (f_new - g0)]
+        wav = self._generate_window(self.codes[g0 - self.c_off:g1 - self.c_off], final)
+        out = wav[self.hop * (self.emitted - g0):self.hop * (f_new - g0)].clone()
         self.emitted = f_new
         drop = max(0, f_new - self.gen_halo) - self.c_off
         self.codes, self.c_off = self.codes[drop:], self.c_off + drop
@@ -161,6 +246,8 @@ class HaloStream:
         if self.done:
             raise RuntimeError("push after flush")
         chunk = torch.as_tensor(chunk, dtype=torch.float32).to(self.engine.device).reshape(-1)
+        if self.push_samples is not None and chunk.numel() > self.push_samples:
+            raise ValueError(f"chunk of {chunk.numel()} samples exceeds push_samples={self.push_samples}")
         self.audio = torch.cat([self.audio, chunk])
         return self._advance(final=False)
 
