@@ -88,6 +88,7 @@ SIGNATURES = {
     "dcx_resample_poly": (ctypes.c_int, [_P, _I32, _I64, _I64, _P, _I32, _I32, _I32, _I64, _P, _I64, _I64, _P]),
     "dcx_set_gemm_mode": (ctypes.c_int, [_P, _I32]),
     "dcx_get_gemm_mode": (_I32, [_P]),
+    "dcx_set_split_k": (ctypes.c_int, [_P, _I32]),
     "dcx_conv_create": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, ctypes.POINTER(_P)]),
     "dcx_conv_forward": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, _P, _P, _P, _I32, _P]),
     "dcx_conv_destroy": (None, [_P]),

@@ -115,6 +115,10 @@ struct dcx_codec {
   // compact bf16 activations between bf16-mode producers and conv_gemm_bf16dm / vq_prefilter_bk;
   // DCX_NO_COMPACT=1 at dcx_create keeps the planes layout (A/B comparisons, same bits)
   bool compact = true;
+  // split-K latency mode (dcx_set_split_k): at most split_k K-slices per few-tile x6 conv; the
+  // partial sums live in the first kSplitScratch bytes of each stage call's workspace (split_buf)
+  int split_k = 0;
+  float* split_buf = nullptr;
 
   ConvW conv_pre;
   ConvW ups[8];
@@ -603,9 +607,54 @@ double conv_bytes(const ConvW& w, const ConvCall& c) {
   return 4.0 * ((double)c.batch * c.Lin * w.cin + outs + (double)w.phases * w.cout * w.taps * w.cin);
 }
 
+// ---- split-K latency mode --------------------------------------------------------------------
+// A conv whose output fits kSplitMaxOut floats and whose tiles leave most CUs idle (the few-tile
+// kernels) runs as S K-slices over input-channel chunks, each writing fp32 partial sums, and one
+// reduce kernel that sums them in slice order and applies the conv's epilogue.  Summation order
+// (and so the low bits) then depends on S, i.e. on the tile count: the mode is opt-in and a clip
+// alone is not bit-equal to the same clip in a batch.
+constexpr long long kSplitMaxOut = 1LL << 21;        // floats per partial output (8 MiB)
+constexpr int kSplitMax = 16;
+constexpr size_t kSplitScratch = (size_t)kSplitMax * kSplitMaxOut * sizeof(float);
+
+int split_factor(const dcx_codec* h, const ConvW& w, const ConvCall& c, const ConvParams& p) {
+  if (h->split_k < 2 || !h->split_buf || p.nprod != 6 || !p.w6 || !p.x6 || p.x_compact || w.cout % 128) return 1;
+  const long long out = (long long)c.batch * c.Lq * w.out_mul * w.cout;
+  if (out > kSplitMaxOut || !dcx::x6_few_tiles(c.Lq, w.cout, w.phases, (w.taps - 1) * std::abs(w.in_step) > 0) || (w.cin / 16) % (w.taps % 2 ? 2 : 1)) return 1;
+  const long long tiles = (long long)c.batch * ((c.Lq + 255) / 256) * std::max(1, w.cout / 128) * w.phases;
+  const int unit = w.taps % 2 ? 2 : 1;  // chunks per slice: an even number of steps per slice
+  const long long nunits = (w.cin / 16) / unit;
+  return (int)std::min<long long>({(long long)std::min(h->split_k, kSplitMax), std::max<long long>(1, 256 / tiles), nunits});
+}
+
+int run_conv_split(dcx_codec* h, const ConvW& w, const ConvCall& c, const ConvParams& p, int S, hipStream_t s) {
+  ProfScope ps(h, s);
+  // one launch: slice sl of clip b is virtual clip sl * batch + b, its partial sums at that clip's
+  // place in split_buf; then one reduce launch applies the epilogue
+  ConvParams q = p;
+  q.ksplit = S;
+  q.kunit = w.taps % 2 ? 2 : 1;
+  q.bias = q.gamma = q.res = nullptr;
+  q.macc = nullptr;
+  q.y = h->split_buf;
+  q.y2 = nullptr;
+  q.y6 = q.y6s = nullptr;
+  q.epi = dcx::EPI_BIAS;
+  q.mean_mode = dcx::MEAN_NONE;
+  q.y_compact = 0;
+  q.round_bf16 = 0;
+  const char* kname = "conv";
+  HIPCHK(h, dcx::launch_conv(q, c.batch * S, w.phases, s, &kname));
+  HIPCHK(h, dcx::launch_splitk_epilogue(p, h->split_buf, S, (long long)c.batch * p.y_bstride, c.batch, w.phases, s));
+  ps.done((std::string("splitk:") + kname).c_str(), conv_flops(w, c), conv_bytes(w, c));
+  return DCX_OK;
+}
+
 int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, bool force_f32 = false) {
   ConvParams p;
   RUN(conv_params(h, w, c, force_f32, p));
+  const int S = force_f32 ? 1 : split_factor(h, w, c, p);
+  if (S > 1) return run_conv_split(h, w, c, p, S, s);
   ProfScope ps(h, s);
   const char* kname = "conv";
   HIPCHK(h, dcx::launch_conv(p, c.batch, w.phases, s, &kname));
@@ -1322,6 +1371,7 @@ size_t dcx_workspace_size(const dcx_codec* h, int32_t batch, int64_t frames) {
   Bump q(nullptr, 0, true);  // vq_encode with every optional output in the workspace
   stage_vq_encode(hh, CAct(), batch, (int)frames, nullptr, nullptr, nullptr, nullptr, q, 0);
   need = std::max(need, q.off + (size_t)batch * frames * (h->cfg.codebook_dim + h->cfg.vq_dim) * 4 + 1024);
+  if (h->split_k > 1) need += kSplitScratch + 256;  // split-K partial sums (STAGE_PRE)
   return need + 4096;
 }
 
@@ -1330,7 +1380,8 @@ size_t dcx_workspace_size(const dcx_codec* h, int32_t batch, int64_t frames) {
   if (rc_ != DCX_OK) return rc_;                                      \
   if (batch <= 0) return fail(h, DCX_ERR_INVALID_ARG, "batch must be > 0"); \
   hipStream_t s = (hipStream_t)stream;                                \
-  Bump ws(workspace, ws_bytes, false)
+  Bump ws(workspace, ws_bytes, false);                                \
+  h->split_buf = h->split_k > 1 ? (float*)ws.raw(kSplitScratch) : nullptr
 
 int dcx_mel(dcx_codec* h, const float* audio, int32_t batch, int64_t n, float* mel, void* workspace, size_t ws_bytes,
             void* stream) {
@@ -1406,6 +1457,12 @@ int dcx_set_gemm_mode(dcx_codec* h, int32_t mode) {
 }
 
 int32_t dcx_get_gemm_mode(const dcx_codec* h) { return h ? h->gemm_mode : -1; }
+
+int dcx_set_split_k(dcx_codec* h, int32_t max_splits) {
+  if (!h || max_splits < 0 || max_splits > kSplitMax) return DCX_ERR_INVALID_ARG;
+  h->split_k = max_splits;
+  return DCX_OK;
+}
 
 }  // extern "C"
 

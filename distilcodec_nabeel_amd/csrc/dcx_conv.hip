@@ -87,6 +87,22 @@ __device__ __forceinline__ void flat_tile(int tpc, int batch, int& wg, int& b, i
   wg = r - b * tpc;
 }
 
+// Split-K (ConvParams::ksplit > 1): the launch's clips are virtual, b = slice * clips + clip; slice
+// `sl` owns the input-channel chunks [c0, c0 + nchunks) (whole units of kunit chunks, as even as
+// the units allow) and writes its partial sums as clip b of the output (the caller's partial buffer).
+__device__ __forceinline__ void ksplit_slice(const ConvParams& p, int b, int& clip, int& c0, int& nchunks) {
+  clip = b;
+  c0 = 0;
+  nchunks = p.Cin / BK;
+  if (p.ksplit > 1) {
+    const int clips = p.batch / p.ksplit, sl = b / clips;
+    clip = b - sl * clips;
+    const int nunits = nchunks / p.kunit, base = nunits / p.ksplit, extra = nunits % p.ksplit;
+    c0 = (sl * base + min(sl, extra)) * p.kunit;
+    nchunks = (base + (sl < extra ? 1 : 0)) * p.kunit;
+  }
+}
+
 // Zero page read in place of out-of-range input rows (conv zero padding): selecting the address
 // instead of the loaded value keeps every staging load unconditional, so hipcc neither branches
 // around it nor waits vmcnt(0) after it (cdna_hip_programming.md §5, trap 4(c)).
@@ -291,6 +307,69 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
 #pragma unroll
       for (int rb = 0; rb < ROWS_T; rb += IBF) batch(r0, rb, rb == 0, std::integral_constant<int, IBF>{});
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Split-K reduce: v = bias + sum of the K-slices' partial sums (in slice order), then the epilogue
+// of epilogue_lds element by element (one thread per 4 output channels of a row).
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) splitk_epilogue_kernel(const ConvParams p, const float* __restrict__ part,
+                                                              int splits, long long stride, long long total4) {
+  const long long i4 = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i4 >= total4) return;
+  const int c4n = p.Cout / 4;
+  const long long rowi = i4 / c4n;  // (phase, clip, q)
+  const int co = (int)(i4 - rowi * c4n) * 4;
+  const long long per_ph = (long long)p.batch * p.Lq;
+  const int ph = (int)(rowi / per_ph);
+  const long long r2 = rowi - ph * per_ph;
+  const int b = (int)(r2 / p.Lq), q = (int)(r2 - (long long)b * p.Lq);
+  const long long ob = (long long)b * p.y_bstride;
+  const long long orow = (long long)q * p.out_mul + ph;
+  const long long o = ob + orow * p.ldy + co;
+  f32x4 x = *reinterpret_cast<const f32x4*>(part + o);
+  for (int s = 1; s < splits; ++s) x += *reinterpret_cast<const f32x4*>(part + s * stride + o);
+  if (p.bias) x += *reinterpret_cast<const f32x4*>(p.bias + co);
+  if (p.round_bf16) x = round_bf16x4(x);
+  switch (p.epi) {
+    case EPI_GELU:
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = gelu_f(x[e]);
+      if (p.round_bf16) x = round_bf16x4(x);
+      break;
+    case EPI_GAMMA_RES:
+      x = *reinterpret_cast<const f32x4*>(p.res + o) + *reinterpret_cast<const f32x4*>(p.gamma + co) * x;
+      break;
+    case EPI_RES: x = *reinterpret_cast<const f32x4*>(p.res + o) + x; break;
+    case EPI_LOGCLAMP:
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = logf(fmaxf(x[e], 1e-5f));
+      break;
+    default: break;
+  }
+  if (p.mean_mode == MEAN_FIRST) {
+    *reinterpret_cast<f32x4*>(p.macc + o) = x;
+    return;
+  } else if (p.mean_mode == MEAN_MID) {
+    *reinterpret_cast<f32x4*>(p.macc + o) = *reinterpret_cast<const f32x4*>(p.macc + o) + x;
+    return;
+  } else if (p.mean_mode == MEAN_LAST) {
+    x = (*reinterpret_cast<const f32x4*>(p.macc + o) + x) / 3.0f;
+  }
+  if (p.y) *reinterpret_cast<f32x4*>(p.y + o) = x;
+  if (p.y6) {
+    unsigned short* y6 = p.y6 + ob * (p.y_compact == 1 ? 1 : p.y_compact == 2 ? 2 : 3);
+    if (p.y_compact == 1) store_bf16x4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
+    else if (p.y_compact == 2) store_hm4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
+    else store_planes4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
+  }
+  if (p.y2 || p.y6s) {
+    f32x4 sv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sv[e] = silu_f(x[e]);
+    if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
+    if (p.y6s) store_planes4(p.y6s + ob * 3, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
   }
 }
 
@@ -593,6 +672,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) conv_gemm_x6w8(const ConvPara
   const int wm = wave / WN, wn = wave % WN;
   const long long ldx6 = (long long)p.ldx * 3;
   const int nchunks = p.Cin / BK;
+  const int wchunks = nchunks;
   const int taps = p.taps;
   const int nsteps = nchunks * taps;
   const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
@@ -623,7 +703,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) conv_gemm_x6w8(const ConvPara
     row0 = q0 + p.in_base[ph] + lo_rel;
     if constexpr (AF32) xbf = p.x + (long long)b * p.x_bstride;
     else xb6 = p.x6 + (long long)b * p.x_bstride * 3;
-    wbase = p.w6 + ((long long)ph * taps * nchunks) * p.Cout * 48 + (long long)co0 * 48;
+    wbase = p.w6 + ((long long)ph * taps * wchunks) * p.Cout * 48 + (long long)co0 * 48;
   };
   int L = tile_base;
   if (L >= total) return;  // whole workgroup, before any barrier
@@ -698,7 +778,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) conv_gemm_x6w8(const ConvPara
     }
   };
   auto loadB = [&](int c, int m, f32x4(&r)[B_PT]) {
-    const unsigned short* src = wbase + ((long long)m * nchunks + c) * wslab;
+    const unsigned short* src = wbase + ((long long)m * wchunks + c) * wslab;
 #pragma unroll
     for (int i = 0; i < B_PT; ++i) r[i] = *reinterpret_cast<const f32x4*>(src + b_off[i]);
   };
@@ -915,16 +995,18 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
   flat_tile(((p.Lq + BM - 1) / BM) * ntiles, p.batch, wg, b, ph);
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
-  const unsigned short* __restrict__ xb6 = AF32 ? nullptr : p.x6 + (long long)b * p.x_bstride * 3;
-  const float* __restrict__ xbf = AF32 ? p.x + (long long)b * p.x_bstride : nullptr;
+  int clip, c0, nchunks;
+  ksplit_slice(p, b, clip, c0, nchunks);  // split-K slice (AF32 launches never split)
+  const unsigned short* __restrict__ xb6 = AF32 ? nullptr : p.x6 + (long long)clip * p.x_bstride * 3 + c0 * 48;
+  const float* __restrict__ xbf = AF32 ? p.x + (long long)clip * p.x_bstride : nullptr;
   const long long ldx6 = (long long)p.ldx * 3;
-  const int nchunks = p.Cin / BK;
+  const int wchunks = p.Cin / BK;  // weight layout
   const int taps = p.taps;
   const int nsteps = nchunks * taps;
   const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
   const int row0 = q0 + p.in_base[ph] + lo_rel;
   const unsigned short* __restrict__ wbase =
-      p.w6 + ((long long)ph * taps * nchunks) * p.Cout * 48 + (long long)co0 * 48;
+      p.w6 + ((long long)ph * taps * wchunks + c0) * p.Cout * 48 + (long long)co0 * 48;
   const long long wslab = (long long)p.Cout * 48;
   const int lin = p.Lin;
 
@@ -982,7 +1064,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
     }
   };
   auto loadB = [&](int c, int m) {
-    const unsigned short* src = wbase + ((long long)m * nchunks + c) * wslab;
+    const unsigned short* src = wbase + ((long long)m * wchunks + c) * wslab;
 #pragma unroll
     for (int i = 0; i < B_PT; ++i) rb[i] = *reinterpret_cast<const f32x4*>(src + b_off[i]);
   };
@@ -1202,15 +1284,17 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6lm(const ConvParams p) {
   flat_tile(((p.Lq + BM - 1) / BM) * ntiles, p.batch, wg, b, ph);
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
-  const unsigned short* __restrict__ xb6 = p.x6 + (long long)b * p.x_bstride * 3;
+  int clip, c0, nchunks;
+  ksplit_slice(p, b, clip, c0, nchunks);  // split-K slice
+  const unsigned short* __restrict__ xb6 = p.x6 + (long long)clip * p.x_bstride * 3 + c0 * 48;
   const long long ldx6 = (long long)p.ldx * 3;
-  const int nchunks = p.Cin / BK;
+  const int wchunks = p.Cin / BK;  // weight layout
   const int taps = p.taps;
   const int nsteps = nchunks * taps;
   const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
   const int row0 = q0 + p.in_base[ph] + lo_rel;
   const unsigned short* __restrict__ wbase =
-      p.w6 + ((long long)ph * taps * nchunks) * p.Cout * 48 + (long long)co0 * 48;
+      p.w6 + ((long long)ph * taps * wchunks + c0) * p.Cout * 48 + (long long)co0 * 48;
   const long long wslab = (long long)p.Cout * 48;
   const int lin = p.Lin;
 
@@ -1245,7 +1329,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6lm(const ConvParams p) {
       *reinterpret_cast<f32x4*>(lds + buf * ABUF + a_row[i] * XROW + a_k[i] * 8) = r[i];
   };
   auto loadB = [&](int c, int m, f32x4(&r)[B_PT]) {
-    const unsigned short* src = wbase + ((long long)m * nchunks + c) * wslab;
+    const unsigned short* src = wbase + ((long long)m * wchunks + c) * wslab;
 #pragma unroll
     for (int i = 0; i < B_PT; ++i) r[i] = *reinterpret_cast<const f32x4*>(src + b_off[i]);
   };
@@ -2712,6 +2796,26 @@ static hipError_t launch_x6w8_af32(const ConvParams& p, int batch, int phases, h
 
 static int tap_span(const ConvParams& p) { return (p.taps - 1) * (p.in_step < 0 ? -p.in_step : p.in_step); }
 
+bool x6_few_tiles(int lq, int cout, int phases, bool halo) {
+  ConvParams q{};
+  q.Lq = lq;
+  q.Cout = cout;
+  // launch_conv: 1-tap convs take the 64K tiles only as 256 x 256, halo convs as 512 x 128 too
+  return !big_tiles_pay(q, phases, 256) && (!halo || !big_tiles_pay(q, phases, 128));
+}
+
+hipError_t launch_splitk_epilogue(const ConvParams& p, const float* partials, int splits, long long stride, int batch,
+                                  int phases, hipStream_t s) {
+  if (splits < 1 || p.Cout % 4 || p.ldy != p.Cout) return hipErrorInvalidValue;
+  ConvParams q = p;
+  q.batch = batch;
+  q.phases = phases;
+  const long long total4 = (long long)phases * batch * p.Lq * (p.Cout / 4);
+  hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s, q, partials, splits,
+                     stride, total4);
+  return hipGetLastError();
+}
+
 bool bf16dm_takes(int cin, int cout, int lq, int ldx, int phases) {
 #ifdef DCX_NO_BF16DM
   return false;
@@ -2727,6 +2831,11 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
   if (p.Cin % BK || p.Cout % 32 || phases < 1 || phases > kMaxPhases) return hipErrorInvalidValue;
   if (p.w6) {
     if (p.nprod != 6 && p.nprod != 1) return hipErrorInvalidValue;
+    // split-K runs only where conv_gemm_x6pp / x6lm would (the kernels that read ksplit)
+    if (p.ksplit > 1 && (p.nprod != 6 || !p.x6 || p.Cout % 128 || batch % p.ksplit || p.kunit < 1 ||
+                         (p.Cin / BK) % p.kunit || (p.Cin / BK) / p.kunit < p.ksplit ||
+                         !x6_few_tiles(p.Lq, p.Cout, phases, tap_span(p) > 0)))
+      return hipErrorInvalidValue;
     const bool b1 = p.nprod == 1;  // profile names: conv_gemm_bf16w* for the one-product mode
     const int span = tap_span(p);
     if (span > 64 || (p.Cin / BK) * p.taps % 2) return hipErrorInvalidValue;

@@ -68,6 +68,10 @@ struct ConvParams {
   // bf16-mode 1x1 weights as [phase][Cin/32][Cout][32] bf16 (hi only; conv_gemm_bf16dm), or null;
   // for the VQ prefilter: the codebook as launch_repack_codebook_bk writes it.
   const unsigned short* wc;
+  // split-K (conv_gemm_x6pp / x6lm only): ksplit > 1 slices over input-channel chunks, each a
+  // whole number of kunit chunks; batch = clips * ksplit, and slice s of clip c is output clip
+  // s * clips + c (partial sums, plain fp32: launch_splitk_epilogue finishes them)
+  int ksplit, kunit;
 };
 
 // Independent convs issued as one launch (launch_conv_group); problem k owns logical tiles
@@ -105,6 +109,13 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
 // launches them one by one, which gives the same bits).
 hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t s, const char** kname);
 hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** kname);
+// Split-K latency mode: whether an x6 conv of this shape runs on the few-tile kernels
+// (conv_gemm_x6pp / x6lm: the ones that take ConvParams::ksplit), and the reduce
+// kernel that sums `splits` fp32 partial outputs (laid out like p.y, `stride` floats apart, in
+// order) and applies p's whole epilogue (bias, epi, mean, every output and layout).
+bool x6_few_tiles(int lq, int cout, int phases, bool halo);
+hipError_t launch_splitk_epilogue(const ConvParams& p, const float* partials, int splits, long long stride, int batch,
+                                  int phases, hipStream_t s);
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname);
 int vq_argmin_ntiles(int ncodes);
 // per-row partial count of the x6-mode prefilter (launch_vq_prefilter)

@@ -121,6 +121,12 @@ class NativeCodec:
         self._check(self.L.dcx_set_gemm_mode(self.h, GEMM_MODES[mode]))
         self.gemm = mode
 
+    def set_split_k(self, max_splits: int) -> None:
+        """Split-K latency mode (dcx_set_split_k): few-tile convs run as up to `max_splits` K-slices.
+        Opt-in for small batches; results then depend on the tile count (not batch-invariant)."""
+        self._check(self.L.dcx_set_split_k(self.h, int(max_splits)))
+        self._ws = None  # the workspace size changed
+
     def num_frames(self, n_samples: int) -> int:
         return int(self.L.dcx_num_frames(self.h, n_samples))
 

@@ -170,6 +170,14 @@ int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int6
 int dcx_set_gemm_mode(dcx_codec* h, int32_t mode);
 int32_t dcx_get_gemm_mode(const dcx_codec* h);
 
+/* Split-K latency mode for small batches (streaming hops, short clips; BASELINE configs[4]): x6
+ * convs whose output tiles would leave most CUs idle run as up to max_splits (<= 16) K-slices
+ * over input channels plus one reduce kernel that sums the partials in order and applies the
+ * epilogue.  0 or 1 = off (default).  While on, dcx_workspace_size includes 128 MiB of partial
+ * sums, and results depend on the tile count (a clip alone is no longer bit-equal to the same
+ * clip inside a batch; fp32-level differences).  Takes effect for later calls; size workspaces after. */
+int dcx_set_split_k(dcx_codec* h, int32_t max_splits);
+
 /* Standalone 1-D convolution primitive (the kernel family behind every stage), for tests and
  * benchmarks.  weight: host fp32, Conv1d layout [Cout][Cin][k] (transposed=0) or
  * ConvTranspose1d layout [Cin][Cout][k] (transposed=1, padding (k-stride)/2); bias may be NULL.

@@ -57,11 +57,24 @@ def test_halo_stream_equals_full_clip(eng, chunk):
     _check_against_full(eng, x, wav, codes, f"chunk {chunk}")
 
 
+@pytest.fixture(scope="module")
+def eng_split(cfg, state):
+    from distilcodec_nabeel_amd.engine import NativeCodec
+
+    e = NativeCodec(cfg, state, "cuda:0", gemm="x6")
+    e.set_split_k(16)  # the latency mode the C5 numbers are quoted with
+    return e
+
+
+@pytest.mark.parametrize("split", [False, True], ids=["plain", "splitk"])
 @pytest.mark.parametrize("chunk", [24000, 7001])
-def test_graphed_halo_stream(eng, chunk):
+def test_graphed_halo_stream(eng, eng_split, chunk, split):
     """Fixed windows of one shape per push, captured in two HIP graphs: bit-equal to the eager
-    fixed-window run, and equal to the full clip within the bounds above."""
+    fixed-window run, and equal to the full clip within the bounds above (also in the split-K
+    latency mode, whose full-clip reference is the same engine)."""
     from distilcodec_nabeel_amd import streaming, synth
+
+    eng = eng_split if split else eng
 
     clip = synth.clips(1, 6 * 24000 + 301, seed=13, kind="mix")[0].astype(np.float32)
     x = torch.from_numpy(np.concatenate([[0.0], clip]).astype(np.float32)).cuda()

@@ -36,9 +36,12 @@ def main():
     ap.add_argument("--hop-samples", type=int, default=24000)
     ap.add_argument("--gemm", default="x6", choices=["x6", "f32"])
     ap.add_argument("--kernels", default=None, help="also write a per-kernel profile of 10 eager hops (json)")
+    ap.add_argument("--split-k", type=int, default=0, help="split-K latency mode: max K-slices per few-tile conv")
     a = ap.parse_args()
     cfg = config.default_config()
     eng = NativeCodec(cfg, weights.synthetic_state_dict(cfg, seed=1234), "cuda:0", gemm=a.gemm)
+    if a.split_k:
+        eng.set_split_k(a.split_k)
     n = a.hop_samples
     stream = np.concatenate(synth.clips(1, n * (a.hops + a.warmup), seed=3, kind="speech"))
     chunks = torch.from_numpy(stream.reshape(-1, 1, n).astype(np.float32)).cuda()
@@ -81,7 +84,7 @@ def main():
     print(json.dumps({
         "config": "C5: streaming encode->decode, hop %d samples (B=1), one hipGraph-captured step" % n,
         "frames_per_hop": hop.frames, "output_samples_per_hop": eng.hop * hop.frames, "hops": a.hops,
-        "gemm": a.gemm, "eager_ms": stats(eager), "graph_ms": g,
+        "gemm": a.gemm, "split_k": a.split_k, "eager_ms": stats(eager), "graph_ms": g,
         "real_time_factor_p99": round(g["p99"] / hop_ms, 5), "graph_equals_eager": exact,
         "data": "synthetic speech-like audio, seeded synthetic weights",
     }), flush=True)
