@@ -14,7 +14,7 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "distilcodec_nabeel_amd", "csrc")
-DRIVER = os.path.join(CSRC, "build", "asan", "host_driver")
+DRIVER = os.path.join(REPO, "distilcodec_nabeel_amd", "dcx_asan_driver")
 MP3 = os.path.join(REPO, "tests", "golden", "test.mp3")
 
 
