@@ -85,54 +85,81 @@ hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, int y6c,
 }
 
 // ConvNeXtBlock front (convnext_utils.py:266-268): depthwise Conv1d k7 p3 (+bias) then
-// F.layer_norm over channels.  dww is packed [7][C].  One wave per output row.
+// F.layer_norm over channels.  dww is packed [7][C].  A workgroup (4 waves) owns DW_R consecutive
+// rows of one clip: it stages their input rows with the 3-row halo on each side in LDS once (rows
+// outside the clip as zeros: the conv's padding), so each input row is read from memory
+// (R + 6) / R times instead of 7; each wave then finishes every 4th row (taps from LDS, one wave
+// per row for the LayerNorm reduction).  The per-row arithmetic and its order are those of the
+// one-wave-per-row form this replaces (taps in order, out-of-range products dropped).
+constexpr int DW_R = 16;
+
 template <int NV>
 __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                          unsigned short* __restrict__ y6, int y6c,
                                                          const float* __restrict__ dww, const float* __restrict__ dwb,
                                                          const float* __restrict__ lnw, const float* __restrict__ lnb,
-                                                         int L, long long rows) {
-  constexpr int C = 256 * NV;
-  const int lane = threadIdx.x & 63;
-  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const long long bidx = row / L;
-  const int t = (int)(row - bidx * L);
-  const float* xb = x + bidx * (long long)L * C;
-  // all 7 taps' loads unconditional (row clamped, out-of-range products dropped by a select):
-  // loads inside the range branches were each followed by a vmcnt(0), one round trip per tap
-  f32x4 v[NV];
+                                                         int L, int tiles) {
+  constexpr int C = 256 * NV, C4 = C / 4, ROWS = DW_R + 6;
+  __shared__ f32x4 tile[ROWS * C4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bidx = blockIdx.x / tiles, t0 = (blockIdx.x - bidx * tiles) * DW_R;
+  const float* xb = x + (long long)bidx * L * C;
+  // stage rows t0 - 3 .. t0 + DW_R + 2 (all loads issued before any LDS store)
+  constexpr int PER = (ROWS * C4 + 255) / 256;
+  f32x4 st[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = threadIdx.x + k * 256;
+    const int r = i / C4, c4 = i - r * C4;
+    const int tt = t0 - 3 + r;
+    const bool ok = i < ROWS * C4 && tt >= 0 && tt < L;
+    st[k] = ok ? *reinterpret_cast<const f32x4*>(xb + (long long)tt * C + c4 * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = threadIdx.x + k * 256;
+    if (i < ROWS * C4) tile[i] = st[k];
+  }
+  f32x4 wv[NV][7], bv[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (lane + 64 * i) * 4;
-    f32x4 xv[7], wv[7];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      const int tt = min(max(t + j - 3, 0), L - 1);
-      xv[j] = *reinterpret_cast<const f32x4*>(xb + (long long)tt * C + c);
-      wv[j] = *reinterpret_cast<const f32x4*>(dww + j * C + c);
-    }
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      const int tt = t + j - 3;
-      const f32x4 pr = xv[j] * wv[j];
-      if (tt >= 0 && tt < L) acc += pr;
-    }
-    v[i] = acc + *reinterpret_cast<const f32x4*>(dwb + c);
+    for (int j = 0; j < 7; ++j) wv[i][j] = *reinterpret_cast<const f32x4*>(dww + j * C + c);
+    bv[i] = *reinterpret_cast<const f32x4*>(dwb + c);
   }
-  ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y ? y + row * C : nullptr, y6, y6c, row, lane);
+  __syncthreads();
+  for (int rr = wave; rr < DW_R; rr += 4) {
+    const int t = t0 + rr;
+    if (t >= L) break;  // wave-uniform
+    f32x4 v[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        const int tt = t + j - 3;
+        const f32x4 pr = tile[(rr + j) * C4 + c4] * wv[i][j];
+        if (tt >= 0 && tt < L) acc += pr;
+      }
+      v[i] = acc + bv[i];
+    }
+    const long long row = (long long)bidx * L + t;
+    ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y ? y + row * C : nullptr, y6, y6c, row, lane);
+  }
 }
 
 hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6c, const float* dww, const float* dwb,
                             const float* lnw, const float* lnb, int batch, int L, int C, hipStream_t s) {
-  const long long rows = (long long)batch * L;
-  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  const int tiles = (L + DW_R - 1) / DW_R;
+  if ((long long)batch * tiles >= (1LL << 31)) return hipErrorInvalidValue;
+  dim3 grid((unsigned)(batch * tiles)), block(256);
   switch (C) {
-    case 256: hipLaunchKernelGGL(dwconv_ln_kernel<1>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, rows); break;
-    case 512: hipLaunchKernelGGL(dwconv_ln_kernel<2>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, rows); break;
-    case 768: hipLaunchKernelGGL(dwconv_ln_kernel<3>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, rows); break;
-    case 1024: hipLaunchKernelGGL(dwconv_ln_kernel<4>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, rows); break;
+    case 256: hipLaunchKernelGGL(dwconv_ln_kernel<1>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
+    case 512: hipLaunchKernelGGL(dwconv_ln_kernel<2>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
+    case 768: hipLaunchKernelGGL(dwconv_ln_kernel<3>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
+    case 1024: hipLaunchKernelGGL(dwconv_ln_kernel<4>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
