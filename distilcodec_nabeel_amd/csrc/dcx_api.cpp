@@ -824,7 +824,11 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   const long long M = (long long)B * T;
   const int D = c.vq_dim, CD = c.codebook_dim, NC = c.codebook_size;
   const bool x6 = x6_mode(h);
-  const int ntiles = x6 ? dcx::vq_prefilter_ntiles(NC, CD) : dcx::vq_argmin_ntiles(NC);
+  // x_pjt_in layout for the prefilter: compact bf16 (bf16 mode, vq_prefilter_bk), "hm" (x6 mode,
+  // vq_prefilter_dm, more than one row panel) or planes
+  const bool p6c = x6 && h->compact && h->gemm_mode == DCX_GEMM_BF16 && h->codebook_bk;
+  const bool p6hm = x6 && h->compact && h->gemm_mode == DCX_GEMM_X6 && h->codebook_bk && dcx::vq_hm_takes(NC, CD, M);
+  const int ntiles = x6 ? dcx::vq_prefilter_ntiles(NC, CD, M, p6c ? 1 : p6hm ? 2 : 0) : dcx::vq_argmin_ntiles(NC);
   RUN(ensure_planes(h, feat, M, D, ws, s, takes_compact(h, h->vq_down, M)));
   if (feat.c1 && !takes_compact(h, h->vq_down, M)) return fail(h, DCX_ERR_STATE, "internal: compact features");
   float* X = ws.f((size_t)M * D);
@@ -845,9 +849,6 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   RUN(run_conv(h, h->vq_down, cd, s));
   const bool x6c = X6 && takes_compact(h, h->vq_pin, M);
   // bf16 mode: x_pjt_in compact for vq_prefilter_bk (the repacked codebook exists iff it takes the shape)
-  const bool p6c = P6 && h->compact && h->gemm_mode == DCX_GEMM_BF16 && h->codebook_bk;
-  // x6 mode: x_pjt_in in the "hm" layout (hi and mid per 32 channels) for vq_prefilter_dm
-  const bool p6hm = P6 && h->compact && h->gemm_mode == DCX_GEMM_X6 && h->codebook_bk && dcx::vq_hm_takes(NC, CD);
   RUN(run_block(h, h->vq_down_blk, X, X6, B, T, ln, hid, s, x6c));
   ConvCall cp = pointwise(CAct(X, X6, x6c), M);
   cp.y = P;

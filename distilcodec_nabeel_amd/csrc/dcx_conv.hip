@@ -2980,7 +2980,14 @@ static bool vq_dm_ok(int ncodes, int dim) {
   return ncodes % (256 * 16) == 0 && dim % BK == 0 && dim / BK >= 3 && (long long)dim * 6 * 256 < (1ll << 31) &&
          (long long)(dim / BK) * ncodes * 96 < (1ll << 31);
 }
-int vq_prefilter_ntiles(int ncodes, int dim) { return ncodes / (vq_dm_ok(ncodes, dim) ? 256 : 128); }
+// Code tile of the prefilter launch_vq_prefilter picks: 256 for vq_prefilter_bk / vq_prefilter_dm, 128
+// for vq_prefilter_x3 (planes x_pjt_in where vq_prefilter_dm's limits fail).  (Routing searches of one
+// row panel, a streaming hop, to the 128-code tiles for twice the workgroups measured 1.55 -> 2.55 ms.)
+int vq_prefilter_ntiles(int ncodes, int dim, long long rows, int x_layout) {
+  (void)rows;
+  if (x_layout == 1 || x_layout == 2) return ncodes / 256;
+  return ncodes / (vq_dm_ok(ncodes, dim) ? 256 : 128);
+}
 
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname) {
   if (p.Cin % BK || p.Cout % 128) return hipErrorInvalidValue;
@@ -3006,7 +3013,10 @@ bool vq_bk_takes(int ncodes, int dim) {
          (long long)(dim / 32) * ncodes * 128 < (1ll << 31);
 }
 
-bool vq_hm_takes(int ncodes, int dim) { return vq_bk_takes(ncodes, dim) && vq_dm_ok(ncodes, dim); }
+bool vq_hm_takes(int ncodes, int dim, long long rows) {
+  (void)rows;
+  return vq_bk_takes(ncodes, dim) && vq_dm_ok(ncodes, dim);
+}
 
 hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipStream_t s, const char** kname) {
   constexpr int BM = 256, BN = 128;
@@ -3016,7 +3026,7 @@ hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipSt
   q.Lin = rows;
   q.taps = 1;
   if (p.x_compact == 2) {  // x6 mode, "hm" x_pjt_in and the repacked codebook: vq_prefilter_dm
-    if (x_bf16 || !p.wc || !vq_hm_takes(p.Cout, p.Cin)) return hipErrorInvalidValue;
+    if (x_bf16 || !p.wc || !vq_hm_takes(p.Cout, p.Cin, rows)) return hipErrorInvalidValue;
     const int mtiles = (rows + 255) / 256, ntiles = p.Cout / 256;
     const dim3 grid((unsigned)(((mtiles + 15) / 16) * (ntiles / 16) * 256));
     if (kname) *kname = "vq_prefilter_dm<256,256>";

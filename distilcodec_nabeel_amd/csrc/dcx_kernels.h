@@ -118,8 +118,9 @@ hipError_t launch_splitk_epilogue(const ConvParams& p, const float* partials, in
                                   int phases, hipStream_t s);
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname);
 int vq_argmin_ntiles(int ncodes);
-// per-row partial count of the x6-mode prefilter (launch_vq_prefilter)
-int vq_prefilter_ntiles(int ncodes, int dim);
+// per-row partial count of the x6 / bf16-mode prefilter launch_vq_prefilter runs for `rows` rows with
+// x_pjt_in in layout x_layout (ConvParams::x_compact)
+int vq_prefilter_ntiles(int ncodes, int dim, long long rows, int x_layout);
 // VQ search, x6 mode: bf16x3 prefilter (approximate squared distances, per-tile top 2) ...
 // x_bf16: the rows of x are bf16 values (mid and lo planes zero), which drops the mid*hi product.
 // p.x_compact == 1 (bf16 mode) / 2 (x6 mode, "hm" layout) with p.wc the launch_repack_codebook_bk
@@ -146,8 +147,8 @@ hipError_t launch_repack_codebook_bk(const unsigned short* cb6, int ncodes, int 
 bool bf16dm_takes(int cin, int cout, int lq, int ldx, int phases);
 // whether vq_prefilter_bk takes the bf16-mode search (then x_pjt_in may be compact)
 bool vq_bk_takes(int ncodes, int dim);
-// whether vq_prefilter_dm takes the x6-mode search with x_pjt_in in the "hm" layout
-bool vq_hm_takes(int ncodes, int dim);
+// whether vq_prefilter_dm takes the x6-mode search of `rows` rows with x_pjt_in in the "hm" layout
+bool vq_hm_takes(int ncodes, int dim, long long rows);
 hipError_t launch_frame_pad(const float* audio, float* frames, unsigned short* frames6, int batch, long long n, int rows,
                             int hop, int pad_left, hipStream_t s);
 hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, long long rows, int nbins, int ld_out,

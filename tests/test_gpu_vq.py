@@ -134,3 +134,15 @@ def test_hm_layout_same_codes(veng, cfg, state):
     assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
     np.testing.assert_array_equal(a[0].cpu().numpy().reshape(-1), _argmin_fp64(a[1].reshape(-1, a[1].shape[-1]),
                                                                                  torch.from_numpy(state["quantizer"][KEY][0])))
+
+
+@pytest.mark.parametrize("rows", [1, 93, 139, 256, 257])
+def test_search_exact_single_row_panel(veng, state, rows):
+    """Searches of at most one 256-row panel (a streaming hop: most of each tile's rows are past the
+    end) and just over one: exact."""
+    from oracle import reference_cpu as R
+
+    g = torch.Generator().manual_seed(rows)
+    feat = torch.randn(1, rows, 1024, generator=g) * 0.5
+    codes, pin = _search(veng, feat)
+    assert np.array_equal(codes, _argmin_fp64(pin, R.codebook(state["quantizer"])))
