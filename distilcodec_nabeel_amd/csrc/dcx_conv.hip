@@ -2236,6 +2236,27 @@ static hipError_t launch_x6dm(const ConvParams& p, int batch, int phases, hipStr
   return hipGetLastError();
 }
 
+// Tile order of the VQ prefilters.  From 16 row panels on, groups of 16 row panels x 16 code tiles
+// are resident together, 4 x 8 per XCD, so the blocks of an XCD stream the same panels through its
+// L2 (ntiles % 16 == 0; grid vq_grid).  Below 16 row panels (short clips, a streaming hop) that
+// order would leave most XCDs without work (a single row panel: two of eight), so the tiles are
+// dealt round-robin over the blocks, code tiles spread over every XCD.  The order changes no result.
+__device__ __forceinline__ void vq_tile(int mtiles, int ntiles, int& mt, int& nt) {
+  const int bid = blockIdx.x;
+  if (mtiles < 16) {
+    mt = bid % mtiles;
+    nt = bid / mtiles;
+    return;
+  }
+  const int xc = bid & 7, l = (bid >> 3) & 31, sup = bid >> 8;
+  const int nsm = (mtiles + 15) >> 4;
+  mt = (sup % nsm) * 16 + (xc & 3) * 4 + (l & 3);
+  nt = (sup / nsm) * 16 + (xc >> 2) * 8 + (l >> 2);
+}
+static unsigned vq_grid(int mtiles, int ntiles) {
+  return mtiles < 16 ? (unsigned)(mtiles * ntiles) : (unsigned)(((mtiles + 15) / 16) * (ntiles / 16) * 256);
+}
+
 // ---------------------------------------------------------------------------------------------
 // VQ prefilter GEMM (x6 mode): approximate x.e from hi*hi + hi*mid + mid*hi of the planes
 // (bound in launch_vq_prefilter), per-tile top 2 of (x2 + e2) - 2 x.e (epilogue_top2).
@@ -2266,10 +2287,8 @@ __global__ void __launch_bounds__(512) vq_prefilter_x3(const ConvParams p) {
   const int ntiles = p.Cout / BN;
   // grouped order: 16 row panels x 16 code tiles resident together, 4 x 8 per XCD (ntiles % 16 == 0)
   const int mtiles = (p.Lq + BM - 1) / BM;
-  const int bid = blockIdx.x, xc = bid & 7, l = (bid >> 3) & 31, sup = bid >> 8;
-  const int nsm = (mtiles + 15) >> 4;
-  const int mt = (sup % nsm) * 16 + (xc & 3) * 4 + (l & 3);
-  const int nt = (sup / nsm) * 16 + (xc >> 2) * 8 + (l >> 2);
+  int mt, nt;
+  vq_tile(mtiles, ntiles, mt, nt);
   if (mt >= mtiles) return;  // whole workgroup, before any barrier
     const int q0 = mt * BM, co0 = nt * BN;
   const int nsteps = p.Cin / 32;
@@ -2451,10 +2470,8 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_dm(const ConvParams p) {
   // grouped order (as vq_prefilter_x3): 16 row panels x 16 code tiles resident together, 4 x 8 per
   // XCD, so the blocks of one XCD stream the same panels through its L2 (ntiles % 16 == 0)
   const int ntiles = p.Cout / BN, mtiles = (p.Lq + BM - 1) / BM;
-  const int bid = blockIdx.x, xc = bid & 7, l = (bid >> 3) & 31, sup = bid >> 8;
-  const int nsm = (mtiles + 15) >> 4;
-  const int mt = (sup % nsm) * 16 + (xc & 3) * 4 + (l & 3);
-  const int nt = (sup / nsm) * 16 + (xc >> 2) * 8 + (l >> 2);
+  int mt, nt;
+  vq_tile(mtiles, ntiles, mt, nt);
   if (mt >= mtiles) return;  // whole workgroup, before any barrier
   const int q0 = mt * BM, co0 = nt * BN;
   const int nsteps = p.Cin / BK;
@@ -2624,10 +2641,8 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_bk(const ConvParams p) {
   const int wm = wave >> 1, wn = wave & 1;
   // grouped order of vq_prefilter_dm: 16 row panels x 16 code tiles resident together
   const int ntiles = p.Cout / BN, mtiles = (p.Lq + BM - 1) / BM;
-  const int bid = blockIdx.x, xc = bid & 7, l = (bid >> 3) & 31, sup = bid >> 8;
-  const int nsm = (mtiles + 15) >> 4;
-  const int mt = (sup % nsm) * 16 + (xc & 3) * 4 + (l & 3);
-  const int nt = (sup / nsm) * 16 + (xc >> 2) * 8 + (l >> 2);
+  int mt, nt;
+  vq_tile(mtiles, ntiles, mt, nt);
   if (mt >= mtiles) return;  // whole workgroup, before any barrier
   const int q0 = mt * BM, co0 = nt * BN;
   const int nsteps = p.Cin / 32;
@@ -3028,7 +3043,7 @@ hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipSt
   if (p.x_compact == 2) {  // x6 mode, "hm" x_pjt_in and the repacked codebook: vq_prefilter_dm
     if (x_bf16 || !p.wc || !vq_hm_takes(p.Cout, p.Cin, rows)) return hipErrorInvalidValue;
     const int mtiles = (rows + 255) / 256, ntiles = p.Cout / 256;
-    const dim3 grid((unsigned)(((mtiles + 15) / 16) * (ntiles / 16) * 256));
+    const dim3 grid(vq_grid(mtiles, ntiles));
     if (kname) *kname = "vq_prefilter_dm<256,256>";
     hipLaunchKernelGGL((vq_prefilter_dm<true>), grid, dim3(512), 0, s, q);
     return hipGetLastError();
@@ -3036,14 +3051,14 @@ hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipSt
   if (p.x_compact == 1) {  // bf16 mode, compact x_pjt_in and the repacked codebook
     if (!x_bf16 || !p.wc || !vq_bk_takes(p.Cout, p.Cin)) return hipErrorInvalidValue;
     const int mtiles = (rows + 255) / 256, ntiles = p.Cout / 256;
-    const dim3 grid((unsigned)(((mtiles + 15) / 16) * (ntiles / 16) * 256));
+    const dim3 grid(vq_grid(mtiles, ntiles));
     if (kname) *kname = "vq_prefilter_bk<256,256>";
     hipLaunchKernelGGL(vq_prefilter_bk, grid, dim3(512), 0, s, q);
     return hipGetLastError();
   }
   if (vq_dm_ok(p.Cout, p.Cin)) {
     const int mtiles = (rows + 255) / 256, ntiles = p.Cout / 256;
-    const dim3 grid((unsigned)(((mtiles + 15) / 16) * (ntiles / 16) * 256));
+    const dim3 grid(vq_grid(mtiles, ntiles));
     if (kname) *kname = x_bf16 ? "vq_prefilter_dm_x2<256,256>" : "vq_prefilter_dm<256,256>";
     if (x_bf16) hipLaunchKernelGGL((vq_prefilter_dm<false>), grid, dim3(512), 0, s, q);
     else hipLaunchKernelGGL((vq_prefilter_dm<true>), grid, dim3(512), 0, s, q);
@@ -3051,7 +3066,8 @@ hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipSt
   }
   const int mtiles = (rows + BM - 1) / BM, ntiles = p.Cout / BN;
   const int nsm = (mtiles + 15) / 16;
-  dim3 grid((unsigned)(nsm * (ntiles / 16) * 256));
+  dim3 grid(vq_grid(mtiles, ntiles));
+  (void)nsm;
   if (p.Cin % 64) return hipErrorInvalidValue;  // even number of K32 steps
   if (x_bf16) {
     if (kname) *kname = "vq_prefilter_x2<256,128>";
