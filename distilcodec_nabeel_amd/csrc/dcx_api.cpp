@@ -620,8 +620,11 @@ constexpr size_t kSplitScratch = (size_t)kSplitMax * kSplitMaxOut * sizeof(float
 int split_factor(const dcx_codec* h, const ConvW& w, const ConvCall& c, const ConvParams& p) {
   if (h->split_k < 2 || !h->split_buf || p.nprod != 6 || !p.w6 || !p.x6 || p.x_compact || w.cout % 128) return 1;
   const long long out = (long long)c.batch * c.Lq * w.out_mul * w.cout;
-  if (out > kSplitMaxOut || !dcx::x6_few_tiles(c.Lq, w.cout, w.phases, (w.taps - 1) * std::abs(w.in_step) > 0) || (w.cin / 16) % (w.taps % 2 ? 2 : 1)) return 1;
+  if (out > kSplitMaxOut || (w.cin / 16) % (w.taps % 2 ? 2 : 1)) return 1;
+  // tiles of the 256 x 128 kernels the slices run on (conv_gemm_x6pp / x6lm, whatever the big-tile
+  // rule would pick unsplit: in this mode the bits depend on the split anyway)
   const long long tiles = (long long)c.batch * ((c.Lq + 255) / 256) * std::max(1, w.cout / 128) * w.phases;
+  if (tiles >= 128) return 1;
   const int unit = w.taps % 2 ? 2 : 1;  // chunks per slice: an even number of steps per slice
   const long long nunits = (w.cin / 16) / unit;
   return (int)std::min<long long>({(long long)std::min(h->split_k, kSplitMax), std::max<long long>(1, 256 / tiles), nunits});

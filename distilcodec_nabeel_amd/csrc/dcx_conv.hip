@@ -2811,14 +2811,6 @@ static hipError_t launch_x6w8_af32(const ConvParams& p, int batch, int phases, h
 
 static int tap_span(const ConvParams& p) { return (p.taps - 1) * (p.in_step < 0 ? -p.in_step : p.in_step); }
 
-bool x6_few_tiles(int lq, int cout, int phases, bool halo) {
-  ConvParams q{};
-  q.Lq = lq;
-  q.Cout = cout;
-  // launch_conv: 1-tap convs take the 64K tiles only as 256 x 256, halo convs as 512 x 128 too
-  return !big_tiles_pay(q, phases, 256) && (!halo || !big_tiles_pay(q, phases, 128));
-}
-
 hipError_t launch_splitk_epilogue(const ConvParams& p, const float* partials, int splits, long long stride, int batch,
                                   int phases, hipStream_t s) {
   if (splits < 1 || p.Cout % 4 || p.ldy != p.Cout) return hipErrorInvalidValue;
@@ -2846,10 +2838,10 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
   if (p.Cin % BK || p.Cout % 32 || phases < 1 || phases > kMaxPhases) return hipErrorInvalidValue;
   if (p.w6) {
     if (p.nprod != 6 && p.nprod != 1) return hipErrorInvalidValue;
-    // split-K runs only where conv_gemm_x6pp / x6lm would (the kernels that read ksplit)
-    if (p.ksplit > 1 && (p.nprod != 6 || !p.x6 || p.Cout % 128 || batch % p.ksplit || p.kunit < 1 ||
-                         (p.Cin / BK) % p.kunit || (p.Cin / BK) / p.kunit < p.ksplit ||
-                         !x6_few_tiles(p.Lq, p.Cout, phases, tap_span(p) > 0)))
+    // split-K runs on conv_gemm_x6pp / x6lm (the kernels that read ksplit), whatever the tile count
+    const bool ks = p.ksplit > 1;
+    if (ks && (p.nprod != 6 || !p.x6 || p.Cout % 128 || batch % p.ksplit || p.kunit < 1 || (p.Cin / BK) % p.kunit ||
+               (p.Cin / BK) / p.kunit < p.ksplit))
       return hipErrorInvalidValue;
     const bool b1 = p.nprod == 1;  // profile names: conv_gemm_bf16w* for the one-product mode
     const int span = tap_span(p);
@@ -2879,7 +2871,7 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       return launch_x6w8_af32<256, 32, 4, 1, 64>(p, batch, phases, s);
     }
 #ifndef DCX_NO_DM
-    if (!h && x6dm_ok(p, false, 256) && big_tiles_pay(p, phases, 256))
+    if (!ks && !h && x6dm_ok(p, false, 256) && big_tiles_pay(p, phases, 256))
       return launch_x6dm<0, 256>(p, batch, phases, s, kname);  // x6 1-tap, Cout % 256
 #endif
 #ifndef DCX_NO_PP
@@ -2903,7 +2895,7 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       return launch_x6w8<128, 128, 2, 2, 0, false>(p, batch, phases, s);
     }
     if (p.Cout % 128 == 0) {
-      const bool pay256 = big_tiles_pay(p, phases, 256), pay128 = big_tiles_pay(p, phases, 128);
+      const bool pay256 = !ks && big_tiles_pay(p, phases, 256), pay128 = !ks && big_tiles_pay(p, phases, 128);
       (void)pay256;
       (void)pay128;
 #ifndef DCX_NO_DQ

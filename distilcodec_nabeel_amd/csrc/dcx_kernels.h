@@ -109,11 +109,9 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
 // launches them one by one, which gives the same bits).
 hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t s, const char** kname);
 hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** kname);
-// Split-K latency mode: whether an x6 conv of this shape runs on the few-tile kernels
-// (conv_gemm_x6pp / x6lm: the ones that take ConvParams::ksplit), and the reduce
-// kernel that sums `splits` fp32 partial outputs (laid out like p.y, `stride` floats apart, in
-// order) and applies p's whole epilogue (bias, epi, mean, every output and layout).
-bool x6_few_tiles(int lq, int cout, int phases, bool halo);
+// Split-K latency mode: the reduce kernel that sums `splits` fp32 partial outputs of a
+// ConvParams::ksplit launch (laid out like p.y, `stride` floats apart, in order) and applies p's
+// whole epilogue (bias, epi, mean, every output and layout).
 hipError_t launch_splitk_epilogue(const ConvParams& p, const float* partials, int splits, long long stride, int batch,
                                   int phases, hipStream_t s);
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname);
