@@ -91,9 +91,8 @@ hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, int y6c,
 // (R + 6) / R times instead of 7; each wave then finishes every 4th row (taps from LDS, one wave
 // per row for the LayerNorm reduction).  The per-row arithmetic and its order are those of the
 // one-wave-per-row form this replaces (taps in order, out-of-range products dropped).
-constexpr int DW_R = 16;
-
-template <int NV>
+// DW_R = 16 rows per workgroup; 4 when 16-row tiles would leave most CUs idle (a streaming hop).
+template <int NV, int DW_R>
 __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                          unsigned short* __restrict__ y6, int y6c,
                                                          const float* __restrict__ dww, const float* __restrict__ dwb,
@@ -152,14 +151,19 @@ __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict_
 
 hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6c, const float* dww, const float* dwb,
                             const float* lnw, const float* lnb, int batch, int L, int C, hipStream_t s) {
-  const int tiles = (L + DW_R - 1) / DW_R;
+  const bool small = (long long)batch * ((L + 15) / 16) < 512;
+  const int R = small ? 4 : 16, tiles = (L + R - 1) / R;
   if ((long long)batch * tiles >= (1LL << 31)) return hipErrorInvalidValue;
   dim3 grid((unsigned)(batch * tiles)), block(256);
   switch (C) {
-    case 256: hipLaunchKernelGGL(dwconv_ln_kernel<1>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
-    case 512: hipLaunchKernelGGL(dwconv_ln_kernel<2>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
-    case 768: hipLaunchKernelGGL(dwconv_ln_kernel<3>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
-    case 1024: hipLaunchKernelGGL(dwconv_ln_kernel<4>, grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
+    case 256: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<1, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles);
+      else hipLaunchKernelGGL((dwconv_ln_kernel<1, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
+    case 512: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<2, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles);
+      else hipLaunchKernelGGL((dwconv_ln_kernel<2, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
+    case 768: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<3, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles);
+      else hipLaunchKernelGGL((dwconv_ln_kernel<3, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
+    case 1024: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<4, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles);
+      else hipLaunchKernelGGL((dwconv_ln_kernel<4, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
