@@ -79,19 +79,21 @@ def expect(cfg):
     return full, own, (s, e)
 
 
-def test_gloo_world2_oracle_matches_single_process(expect):
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_oracle_matches_single_process(expect, world):
+    """world 2 (shards 3 + 2 clips) and world 4 (2 + 1 + 1 + 1: uneven, single-clip shards)."""
     full, _, _ = expect
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(rk, 2, port, _clips(), q)) for rk in range(2)]
+    procs = [ctx.Process(target=_worker, args=(rk, world, port, _clips(), q)) for rk in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in range(2))
+    res = dict(q.get(timeout=300) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rk in range(2):
+    for rk in range(world):
         assert res[rk].shape == full.shape
         assert np.array_equal(res[rk], full)
 
@@ -107,29 +109,31 @@ def test_global_padding_is_what_matters(expect):
     assert not np.array_equal(full[s + j, :n], own[j])
 
 
-def test_gather_rows_uneven_shards():
-    """gather_rows reassembles unequal shards in rank order (world 3 over 7 rows, gloo)."""
+@pytest.mark.parametrize("world,rows", [(3, 7), (8, 5)])
+def test_gather_rows_uneven_shards(world, rows):
+    """gather_rows reassembles unequal shards in rank order (gloo): world 3 over 7 rows, and world 8
+    over 5 rows, where three ranks hold empty shards."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gather_worker, args=(rk, 3, port, q)) for rk in range(3)]
+    procs = [ctx.Process(target=_gather_worker, args=(rk, world, port, rows, q)) for rk in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(3))
+    res = dict(q.get(timeout=120) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rk in range(3):
-        assert np.array_equal(res[rk], np.arange(7 * 2).reshape(7, 2))
+    for rk in range(world):
+        assert np.array_equal(res[rk], np.arange(rows * 2).reshape(rows, 2))
 
 
-def _gather_worker(rank, world, port, q):
+def _gather_worker(rank, world, port, rows, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        s, e = sharding.shard_bounds(7, rank, world)
+        s, e = sharding.shard_bounds(rows, rank, world)
         local = torch.arange(s * 2, e * 2).reshape(e - s, 2)
-        q.put((rank, sharding.gather_rows(local, 7, world).numpy()))
+        q.put((rank, sharding.gather_rows(local, rows, world).numpy()))
     finally:
         dist.destroy_process_group()
 
