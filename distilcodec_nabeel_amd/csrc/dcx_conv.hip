@@ -2757,6 +2757,207 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_bk(const ConvParams p) {
   epilogue_top2<BM, BN, 4, WN>(p, acc, q0, co0, nt, ntiles, reinterpret_cast<float*>(lds));
 }
 
+// epilogue_top2 for 16x16 accumulator blocks (v_mfma_f32_16x16x32_bf16: lane l holds column
+// l & 15 of its block, rows 4 (l >> 4) + r): the same per-row top 2 and lowest index on ties.
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void epilogue_top2_q(const ConvParams& p, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int q0,
+                                                int co0, int nt, int ntiles, float* smem) {
+  constexpr int WR = BM / WM, WC = BN / WN;
+  constexpr int TM = WR / 16, TN = WC / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lc = lane & 15, r4 = 4 * (lane >> 4);
+  float xxv[TM][4], e2v[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) xxv[i][r] = p.x2[min(q0 + wm * WR + i * 16 + r4 + r, p.Lq - 1)];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) e2v[j] = p.e2[co0 + wn * WC + j * 16 + lc];
+  __syncthreads();
+  float* rv = smem;                                      // [WN][BM]
+  float* rv2 = smem + WN * BM;                           // [WN][BM]
+  int* ri = reinterpret_cast<int*>(smem + 2 * WN * BM);  // [WN][BM]
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rloc = wm * WR + i * 16 + r4 + r;
+      const float xx = xxv[i][r];
+      float v1 = __builtin_inff(), v2 = __builtin_inff();
+      int i1 = 0x7fffffff;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int co = co0 + wn * WC + j * 16 + lc;
+        const float d2 = (xx + e2v[j]) + (-2.0f * acc[i][j][r]);
+        top2_merge(v1, i1, v2, d2, co, __builtin_inff());
+      }
+#pragma unroll
+      for (int off = 8; off >= 1; off >>= 1)
+        top2_merge(v1, i1, v2, __shfl_xor(v1, off, 64), __shfl_xor(i1, off, 64), __shfl_xor(v2, off, 64));
+      if (lc == 0) {
+        rv[wn * BM + rloc] = v1;
+        rv2[wn * BM + rloc] = v2;
+        ri[wn * BM + rloc] = i1;
+      }
+    }
+  }
+  __syncthreads();
+  for (int rloc = tid; rloc < BM; rloc += blockDim.x) {
+    const int q = q0 + rloc;
+    if (q >= p.Lq) continue;
+    float v1 = rv[rloc], v2 = rv2[rloc];
+    int i1 = ri[rloc];
+#pragma unroll
+    for (int w = 1; w < WN; ++w) top2_merge(v1, i1, v2, rv[w * BM + rloc], ri[w * BM + rloc], rv2[w * BM + rloc]);
+    const long long o = (long long)q * ntiles + nt;
+    p.part_val[o] = v1;
+    p.part_val2[o] = v2;
+    p.part_idx[o] = i1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// vq_prefilter_bq: vq_prefilter_bk on v_mfma_f32_16x16x32_bf16 (round 2).
+//
+// Same operands, LDS images, DMA ring and ping-pong schedule as vq_prefilter_bk; only the MFMA
+// shape changes.  The K32 of one 16x16x32 MFMA is split as k = (t, c): t = lane >> 5 picks the
+// codebook plane and c (lane bit 4 and the element) the channel inside a K16 chunk, so one MFMA
+// sums x_h . e_h' + x_h . e_m' over 16 channels, the two products vq_prefilter_bk issues as two
+// 32x32x16 MFMAs.  The product set and the K terms per accumulator are unchanged (each MFMA now
+// adds 32 products instead of 16, half as many MFMAs), so launch_vq_prefilter's bound holds as
+// for vq_prefilter_bk.  Why: under MFMA load the chip holds a higher clock for 16x16x32 than for
+// 32x32x16 at the same cycles per FLOP (MI355X_MICROARCH.md, DVFS; conv_gemm_x6dq).
+// Fragment reads (ds_read_b128, per 16-lane group one 16-byte piece of 16 consecutive rows or
+// codes) are conflict-free under the swizzles of vq_prefilter_bk.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(512, 2) vq_prefilter_bq(const ConvParams p) {
+  constexpr int BM = 256, BN = 256, WN = 2;
+  constexpr int WR = BM / 4, WC = BN / 2, TM = WR / 16, TN = WC / 16;
+  constexpr int ARW = 32, BRW = 64;            // ushorts per LDS row
+  constexpr int A_G = BM * 4 / 64 / 2;         // DMA instructions per group per tile (x: 8)
+  constexpr int B_G = BN * 8 / 64 / 2;         // (codebook: 16)
+  constexpr int A_PW = A_G / 4, B_PW = B_G / 4;  // per wave
+  constexpr int ABUF = BM * ARW, BBUF = BN * BRW;
+  constexpr int LDS_US = 3 * ABUF + 3 * BBUF;  // 144 KiB
+  static_assert(A_G % 4 == 0 && B_G % 4 == 0 && LDS_US * 2 <= 160 * 1024, "tile shape");
+  __shared__ __attribute__((aligned(16))) unsigned short lds[LDS_US];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int group = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntiles = p.Cout / BN, mtiles = (p.Lq + BM - 1) / BM;
+  int mt, nt;
+  vq_tile(mtiles, ntiles, mt, nt);
+  if (mt >= mtiles) return;  // whole workgroup, before any barrier
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int nsteps = p.Cin / 32;
+  const int arow = p.ldx * 2;  // bytes per compact row
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.x6 + (long long)q0 * p.ldx), 0, min(BM, p.Lq - q0) * arow, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wc, 0, nsteps * p.Cout * 128, 0x00020000);
+
+  int a_off[A_PW], b_off[B_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int u = (group * A_G + i * 4 + gw) * 64 + lane;
+    const int row = u >> 2, pc = (u & 3) ^ ((row >> 2) & 3);
+    a_off[i] = row * arow + pc * 16;
+  }
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int u = (group * B_G + i * 4 + gw) * 64 + lane;
+    const int code = u >> 3, pc = (u & 7) ^ ((code >> 1) & 7);
+    b_off[i] = (co0 + code) * 128 + pc * 16;
+  }
+  unsigned short* const a_dst = lds + (group * A_G + gw) * 512;
+  unsigned short* const b_dst = lds + 3 * ABUF + (group * B_G + gw) * 512;
+  auto dma_step = [&](int c, int slot) {
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) dma16(rx, a_dst + slot * ABUF + i * 2048, a_off[i] + c * 64, 0);
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) dma16(rw, b_dst + slot * BBUF + i * 2048, b_off[i], c * p.Cout * 128);
+    return A_PW + B_PW;
+  };
+
+  // lane roles: row / code l & 15 of a 16-block, channel half hh = (l >> 4) & 1, plane t = l >> 5
+  const int l16 = lane & 15, hh = (lane >> 4) & 1, tp = lane >> 5;
+  s16x8 af[TM][2], bfr[TN][2];
+  auto readF = [&](int slot) {
+    const unsigned short* A = lds + slot * ABUF;
+    const unsigned short* Bs = lds + 3 * ABUF + slot * BBUF;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm * WR + i * 16 + l16;
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+        af[i][cc] = *reinterpret_cast<const s16x8*>(A + r * ARW + (((cc * 2 + hh) ^ ((r >> 2) & 3)) << 3));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WC + j * 16 + l16;
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+        bfr[j][cc] = *reinterpret_cast<const s16x8*>(
+            Bs + col * BRW + (((((cc * 2 + hh) * 2) + tp) ^ ((col >> 1) & 7)) << 3));
+    }
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i][cc]),
+                                                              __builtin_bit_cast(bf16x8, bfr[j][cc]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto inc3 = [](int& slot) { slot = slot == 2 ? 0 : slot + 1; };
+
+  for (int t = 0; t < 3; ++t) dma_step(t, t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  seg_barrier();
+  if (group == 0) {
+    readF(0);
+    int rs = 1, ws = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      mfma();  // MFMA(s)
+      seg_barrier();
+      if (s + 1 < nsteps) readF(rs);  // MEM0(s): fragments of step s + 1, issue step s + 3
+      int n = 0;
+      if (s + 3 < nsteps) n = dma_step(s + 3, ws);
+      wait_dma(n);
+      seg_barrier();
+      inc3(rs);
+      inc3(ws);
+    }
+  } else {
+    int rs = 0, ws = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      readF(rs);  // MEM1(s): fragments of step s, issue step s + 2 (s >= 1)
+      int n = 0;
+      if (s >= 1 && s + 2 < nsteps) n = dma_step(s + 2, ws);
+      wait_dma(n);
+      seg_barrier();
+      mfma();  // MFMA(s)
+      seg_barrier();
+      inc3(rs);
+      if (s >= 1) inc3(ws);
+      else ws = 0;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  epilogue_top2_q<BM, BN, 4, WN>(p, acc, q0, co0, nt, ntiles, reinterpret_cast<float*>(lds));
+}
+
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
@@ -3044,8 +3245,13 @@ hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipSt
     if (!x_bf16 || !p.wc || !vq_bk_takes(p.Cout, p.Cin)) return hipErrorInvalidValue;
     const int mtiles = (rows + 255) / 256, ntiles = p.Cout / 256;
     const dim3 grid(vq_grid(mtiles, ntiles));
+#ifdef DCX_VQ_BK32  // the 32x32x16 form (A/B builds)
     if (kname) *kname = "vq_prefilter_bk<256,256>";
     hipLaunchKernelGGL(vq_prefilter_bk, grid, dim3(512), 0, s, q);
+#else
+    if (kname) *kname = "vq_prefilter_bq<256,256>";
+    hipLaunchKernelGGL(vq_prefilter_bq, grid, dim3(512), 0, s, q);
+#endif
     return hipGetLastError();
   }
   if (vq_dm_ok(p.Cout, p.Cin)) {

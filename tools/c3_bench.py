@@ -70,7 +70,7 @@ def main():
         if a.kernels:
             json.dump({"steps": 1, "kernels": kern}, open(f"{a.kernels}_{mode}.json", "w"), indent=1)
         name, rec = max(kern.items(), key=lambda kv: kv[1]["ms"])
-        prods = 2 if "prefilter_bk" in name or "_x2" in name else 3 if "prefilter" in name else 1 if "bf16" in name else 6
+        prods = 2 if "prefilter_bk" in name or "prefilter_bq" in name or "_x2" in name else 3 if "prefilter" in name else 1 if "bf16" in name else 6
         ach = rec["flops"] / (rec["ms"] * 1e-3) / 1e12
         roof = {"bound": "mfma", "kernel": name, "achieved": round(ach, 1), "peak": round(2500.0 / prods, 1),
                 "unit": "TFLOP/s (fp32-equivalent)", "frac": round(ach * prods / 2500.0, 4),

@@ -1,4 +1,4 @@
-# GPU-box: PMC counter passes over the C3 bench (bf16 mode: vq_prefilter_bk, conv_gemm_bf16dm).
+# GPU-box: PMC counter passes over the C3 bench (bf16 mode: vq_prefilter_bq, conv_gemm_bf16dm).
 # Usage: bash tools/gpu_pmc_c3.sh TAG
 set -o pipefail
 TAG=${1:-pmc3}
@@ -13,4 +13,4 @@ for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY
   echo PASS $i ok
 done
 python3 tools/pmc_summary.py $R/gpurun_out/${TAG}_p1 $R/gpurun_out/${TAG}_p2 $R/gpurun_out/${TAG}_p3 > $R/gpurun_out/${TAG}_summary.txt
-grep -A 26 "vq_prefilter_bk\|conv_gemm_bf16dm" $R/gpurun_out/${TAG}_summary.txt | grep -E "^dcx|INSTS|MFMA busy|WAIT|BANK|ACTIVE_INST_ANY /"
+grep -A 26 "vq_prefilter_bq\|vq_prefilter_bk\|conv_gemm_bf16dm" $R/gpurun_out/${TAG}_summary.txt | grep -E "^dcx|INSTS|MFMA busy|WAIT|BANK|ACTIVE_INST_ANY /"
