@@ -66,6 +66,32 @@ __device__ __forceinline__ f32x4 round_bf16x4(f32x4 v) {
   return v;
 }
 __device__ __forceinline__ float gelu_f(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f)); }
+// GELU of the bf16 mode, whose result is rounded to bf16 (2^-8 relative) right after: erf from
+// the Chebyshev-fitted erfc of Numerical Recipes (erfcc, relative error < 1.2e-7 everywhere), one
+// v_rcp_f32, one v_exp_f32 and 9 FMAs, branch-free.  ocml's erff branches on |x| (both paths run in
+// mixed waves) and cost 9 of the 64 ms the bf16 1x1 convs take per C3 step (timing probe).  The x6
+// and fp32 modes keep erff (fp32-accurate GELU).
+__device__ __forceinline__ float gelu_bf16_f(float v) {
+#ifdef DCX_GELU_ERF  // A/B builds: the library erff in the bf16 mode too
+  return gelu_f(v);
+#endif
+  const float z = fabsf(v) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+  float q = 0.17087277f;
+  q = fmaf(q, t, -0.82215223f);
+  q = fmaf(q, t, 1.48851587f);
+  q = fmaf(q, t, -1.13520398f);
+  q = fmaf(q, t, 0.27886807f);
+  q = fmaf(q, t, -0.18628806f);
+  q = fmaf(q, t, 0.09678418f);
+  q = fmaf(q, t, 0.37409196f);
+  q = fmaf(q, t, 1.00002368f);
+  const float c = t * __expf(fmaf(t, q, fmaf(-z, z, -1.26551223f)));  // erfc(|v| / sqrt 2)
+  // erf(v / sqrt 2) rounded to fp32, then the reference's 0.5 v (1 + erf) with its cancellation
+  // for large negative v (torch's GELU formula)
+  const float e = v >= 0.0f ? 1.0f - c : c - 1.0f;
+  return 0.5f * v * (1.0f + e);
+}
 
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
 // blocks b and b+8 share an XCD, so consecutive logical tiles (same row panel, all column
@@ -260,7 +286,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
       switch (p.epi) {
         case EPI_GELU:
 #pragma unroll
-          for (int e = 0; e < 4; ++e) x[e] = gelu_f(x[e]);
+          for (int e = 0; e < 4; ++e) x[e] = p.round_bf16 ? gelu_bf16_f(x[e]) : gelu_f(x[e]);
           if (p.round_bf16) x = round_bf16x4(x);
           break;
         case EPI_GAMMA_RES: x = r[k] + gamma4 * x; break;
@@ -335,7 +361,7 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(const ConvParams p
   switch (p.epi) {
     case EPI_GELU:
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] = gelu_f(x[e]);
+      for (int e = 0; e < 4; ++e) x[e] = p.round_bf16 ? gelu_bf16_f(x[e]) : gelu_f(x[e]);
       if (p.round_bf16) x = round_bf16x4(x);
       break;
     case EPI_GAMMA_RES:

@@ -41,6 +41,30 @@ def test_conv_bf16(case):
     assert float((err > 0).double().mean()) < 0.01
 
 
+@pytest.mark.parametrize("case", [(256, 1024, 1100), (768, 3072, 300)], ids=lambda c: "x".join(map(str, c)))
+def test_conv_gelu_bf16(case):
+    """pwconv1 + GELU in bf16 mode (the encoder's hidden): bf16(gelu(v)) for v = bf16(conv + b) of the
+    same kernel (test_conv_bf16 pins v), with torch's fp32 GELU 0.5 v (1 + erf(v / sqrt 2)), to 1 bf16
+    ulp.  The kernel's branch-free erf (gelu_bf16_f) may differ from torch's erf in the last fp32
+    bits, which moves a bf16 rounding on a small fraction of elements (mostly the cancelling tail
+    v < -2)."""
+    from distilcodec_nabeel_amd.engine import NativeConv
+
+    cin, cout, L = case
+    r = np.random.default_rng(cin)
+    w = (r.standard_normal((cout, cin, 1)) / np.sqrt(cin)).astype(np.float32)
+    b = (0.1 * r.standard_normal(cout)).astype(np.float32)
+    x = (1.5 * r.standard_normal((2, L, cin))).astype(np.float32)
+    conv = NativeConv(w, b)
+    y = conv(torch.from_numpy(x).cuda(), gemm="bf16", epi=1).cpu()
+    pre = conv(torch.from_numpy(x).cuda(), gemm="bf16", epi=0).cpu()  # bf16(conv + b), same kernel
+    ref = _bf(F.gelu(pre))
+    assert torch.equal(y, _bf(y))
+    err = (y.double() - ref.double()).abs()
+    assert bool((err <= 2.0 ** -7 * ref.double().abs() + 1e-6 * ref.double().abs().max()).all())
+    assert float((err > 0).double().mean()) < 0.02
+
+
 @pytest.fixture(scope="module")
 def beng(cfg, state):
     from distilcodec_nabeel_amd.engine import NativeCodec
@@ -96,7 +120,7 @@ def test_codec_flag_switches_and_restores(codec, golden):
 
 @pytest.mark.parametrize("B,secs", [(2, 3), (4, 11)])
 def test_compact_layout_same_bits(beng, cfg, state, B, secs):
-    """bf16 mode stores the activations read by conv_gemm_bf16dm and vq_prefilter_bk in the compact
+    """bf16 mode stores the activations read by conv_gemm_bf16dm and vq_prefilter_bq in the compact
     layout (hi plane only, 2 B per element).  The GEMMs read the same hi values either way, so the
     encoder features and x_pjt_in equal the planes-layout run (DCX_NO_COMPACT=1) bit for bit, and the
     codes too (both exact argmins).  4 x 11 s puts every 1x1 conv on conv_gemm_bf16dm; 2 x 3 s mixes
