@@ -5,7 +5,7 @@ Restates `DistilCodec.construct_audio_code` (distilcodec/distil_codec.py:200-265
 `{'content': '<|g{g}r{r}_{n+offset}|>', 'absolute_token_id': n + offset, 'in_codebook_id': n}`.
 The offset advances by one codebook size per GROUP, not per (group, residual): in the reference the
 `code_index_diff += codebook_size` sits after the residual loop (:219), so the residual codebooks of
-one group share an id range (reproduced as is).  The table ends with by 8 special audio tokens whose ids 5-7 carry the
+one group share an id range (reproduced as is).  The table ends with 8 special audio tokens whose ids 5-7 carry the
 reference's +7/+8/+9 absolute ids (kept verbatim, :253-262).
 """
 from __future__ import annotations
