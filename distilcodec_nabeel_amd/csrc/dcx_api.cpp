@@ -878,8 +878,8 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
     }
   }
   if (x6)
-    LAUNCH(h, s, "vq_rescore", 0, 12.0 * M * ntiles + 4.0 * M * CD,
-           dcx::launch_vq_rescore(pv, pi, pv2, M, ntiles, NC / ntiles, P, CD, h->codebook, h->emax, h->e2max,
+    LAUNCH(h, s, "vq_rescore", 0, 12.0 * M * ntiles + 4.0 * M,
+           dcx::launch_vq_rescore(pv, pi, pv2, M, ntiles, NC / ntiles, P, x2, CD, h->codebook, h->emax, h->e2max,
                                   dcx::kVqPrefilterBound, codes, h->vq_stats, s));
   else
     LAUNCH(h, s, "vq_reduce", 0, 8.0 * M * ntiles, dcx::launch_vq_reduce(pv, pi, (int)M, ntiles, codes, s));

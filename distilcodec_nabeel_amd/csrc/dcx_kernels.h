@@ -128,8 +128,9 @@ hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipSt
 // candidate inside the bound in fp64.  stats (optional): [0] rows rescored, [1] codes rescored.
 constexpr float kVqPrefilterBound = 2.5e-4f;
 hipError_t launch_vq_rescore(const float* part_val, const int* part_idx, const float* part_val2, long long rows,
-                             int ntiles, int tile_codes, const float* x, int dim, const float* codebook, float emax,
-                             float e2max, float cbound, int32_t* codes, int* stats, hipStream_t s);
+                             int ntiles, int tile_codes, const float* x, const float* x2, int dim,
+                             const float* codebook, float emax, float e2max, float cbound, int32_t* codes, int* stats,
+                             hipStream_t s);
 hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows, int ntiles, int32_t* codes,
                             hipStream_t s);
 hipError_t launch_row_sqnorm(const float* x, long long rows, int C, float* out, hipStream_t s);

@@ -333,7 +333,8 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 
 __global__ void __launch_bounds__(256) vq_rescore_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
                                                          const float* __restrict__ pv2, int ntiles, int tile_codes,
-                                                         const float* __restrict__ x, int dim,
+                                                         const float* __restrict__ x,
+                                                         const float* __restrict__ x2, int dim,
                                                          const float* __restrict__ code, float emax, float e2max,
                                                          float cbound, int32_t* __restrict__ codes,
                                                          int* __restrict__ stats) {
@@ -348,7 +349,9 @@ __global__ void __launch_bounds__(256) vq_rescore_kernel(const float* __restrict
   const float* v2p = pv2 + row * ntiles;
   const int* i1p = pi + row * ntiles;
 
-  // 1. best approximate value, and |x|^2 in fp64 (x held in registers for the rescore)
+  // 1. best approximate value.  The bound takes |x|^2 from row_sqnorm (fp64 sum rounded to fp32,
+  // within 2^-24 relative), raised by 2^-20 so it is never below the exact value; the x row itself
+  // (14 KiB at 3584 channels) is read only by rows that go on to the rescore (~10 %).
   float bv = __builtin_inff();
   int bi = 0x7fffffff;
   for (int t = tid; t < ntiles; t += 256) {
@@ -356,17 +359,7 @@ __global__ void __launch_bounds__(256) vq_rescore_kernel(const float* __restrict
     const int i = i1p[t];
     if (v < bv || (v == bv && i < bi)) { bv = v; bi = i; }
   }
-  const int nvec = dim >> 8;  // float4 per lane
-  f32x4 xr[kMaxVqDimVec];
-  double xx = 0;
-  const float* xrow = x + row * dim;
-#pragma unroll
-  for (int u = 0; u < kMaxVqDimVec; ++u) {
-    xr[u] = u < nvec ? *reinterpret_cast<const f32x4*>(xrow + u * 256 + lane * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-    xx += (double)xr[u][0] * xr[u][0] + (double)xr[u][1] * xr[u][1] + (double)xr[u][2] * xr[u][2] +
-          (double)xr[u][3] * xr[u][3];
-  }
-  xx = wave_sum_f64(xx);  // every wave holds the whole row
+  const double xxb = (double)x2[row] * (1.0 + 0x1p-20);
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     const float ov = __shfl_xor(bv, off, 64);
@@ -382,7 +375,7 @@ __global__ void __launch_bounds__(256) vq_rescore_kernel(const float* __restrict
     if (s_v[w] < bv || (s_v[w] == bv && s_i[w] < bi)) { bv = s_v[w]; bi = s_i[w]; }
 
   // 2. candidates inside the bound
-  const double bound = 2.0 * (double)cbound * sqrt(xx) * (double)emax + 8.0 * 0x1p-24 * (xx + (double)e2max);
+  const double bound = 2.0 * (double)cbound * sqrt(xxb) * (double)emax + 8.0 * 0x1p-24 * (xxb + (double)e2max);
   const double thr = (double)bv + 2.0 * bound * (1.0 + 1e-6);
   int cnt = 0;
   for (int t = tid; t < ntiles; t += 256) {
@@ -405,7 +398,19 @@ __global__ void __launch_bounds__(256) vq_rescore_kernel(const float* __restrict
     atomicAdd(&stats[1], cnt);
   }
 
-  // 3. exact rescore of the candidates, one code per wave at a time
+  // 3. exact rescore of the candidates, one code per wave at a time; x and |x|^2 in fp64 (every
+  // wave holds the whole row)
+  const int nvec = dim >> 8;  // float4 per lane
+  f32x4 xr[kMaxVqDimVec];
+  double xx = 0;
+  const float* xrow = x + row * dim;
+#pragma unroll
+  for (int u = 0; u < kMaxVqDimVec; ++u) {
+    xr[u] = u < nvec ? *reinterpret_cast<const f32x4*>(xrow + u * 256 + lane * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    xx += (double)xr[u][0] * xr[u][0] + (double)xr[u][1] * xr[u][1] + (double)xr[u][2] * xr[u][2] +
+          (double)xr[u][3] * xr[u][3];
+  }
+  xx = wave_sum_f64(xx);
   double best = __builtin_inf();
   int bc = 0x7fffffff;
   auto eval = [&](int c) {
@@ -447,13 +452,14 @@ __global__ void __launch_bounds__(256) vq_rescore_kernel(const float* __restrict
 }
 
 hipError_t launch_vq_rescore(const float* part_val, const int* part_idx, const float* part_val2, long long rows,
-                             int ntiles, int tile_codes, const float* x, int dim, const float* codebook, float emax,
-                             float e2max, float cbound, int32_t* codes, int* stats, hipStream_t s) {
+                             int ntiles, int tile_codes, const float* x, const float* x2, int dim,
+                             const float* codebook, float emax, float e2max, float cbound, int32_t* codes, int* stats,
+                             hipStream_t s) {
   if (ntiles < 1 || ntiles > kMaxVqTiles || dim % 256 || dim > 256 * kMaxVqDimVec || rows < 0)
     return hipErrorInvalidValue;
   if (rows == 0) return hipSuccess;
   hipLaunchKernelGGL(vq_rescore_kernel, dim3((unsigned)rows), dim3(256), 0, s, part_val, part_idx, part_val2, ntiles,
-                     tile_codes, x, dim, codebook, emax, e2max, cbound, codes, stats);
+                     tile_codes, x, x2, dim, codebook, emax, e2max, cbound, codes, stats);
   return hipGetLastError();
 }
 
