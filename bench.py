@@ -13,8 +13,14 @@ Workloads (BASELINE.json configs):
 Both run through the shipped multi-GPU path (`sharding.ShardedEncodeDecode`): rank r holds its
 contiguous shard of the global clip list, resident in HBM; a step = `dcx_encode_decode` over the
 shard plus the all_gather of every rank's codes (RCCL over xGMI).  Clips are independent, so there
-is no collective on the data path (weak scaling); the gather is the only exchange.  With N > 1 and
-the default c2 workload, a C4 pass is measured too and reported under "c4".
+is no collective on the data path (weak scaling); the gather is the only exchange.  With the
+default c2 workload the same line carries sub-records (each skippable by a flag):
+  "c4"             a C4 pass (128 ragged clips per GPU, padded to the global max), at every N;
+  "c3"             (N = 1) configs[2]: encoder + GRFVQ token extraction, 256 x 10 s, bf16;
+  "c5"             (N = 1) configs[4]: 1 s hops through one captured hipGraph (split-K latency mode);
+  "codes_vs_oracle" (N = 1) clip 0 of the timed C2 batch against the CPU oracle: decisive codes
+                   exact, the raw code match rate and the waveform SNR (the metric's "code-index
+                   bit-exact vs CPU" clause, measured on the benchmarked workload).
 
 Rank 0 prints one JSON line.  `value` counts real (unpadded) clip samples of all ranks per second.
 `roofline` reports the dominant kernel (largest summed device time, HIP events around each launch
@@ -32,6 +38,7 @@ import statistics
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -49,6 +56,7 @@ X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
 HBM_PEAK_GBS = 8000.0
 SR = 24000
 MFLOP_PER_FRAME = 2045.08  # encode -> decode algorithmic work per 256-sample frame
+C3_MFLOP_PER_FRAME = 415.36  # encode-only (mel excluded) per frame
 
 WORKLOADS = {
     # clips per GPU, longest clip, shortest clip
@@ -116,6 +124,120 @@ def cpu_baseline(cfg, state):
                        f"1 thread on 1 x 1 s clip (runs {', '.join(f'{r:.2f}' for r in runs_one)} s)")}
 
 
+def c3_record(cfg, state, dev, steps: int = 3, batch: int = 256):
+    """BASELINE configs[2] (C3): mel -> encoder -> GRFVQ codes of 256 x 10 s clips in bf16 (the
+    reference's enable_bfloat16), inputs resident in HBM, codes only; one warm-up step, `steps`
+    timed with HIP events; the dominant kernel (HIP events per launch, one more step) against the
+    dense bf16 MFMA peak and against its own product-count ceiling."""
+    n = 10 * SR
+    audio = torch.zeros(batch, n + 1)
+    for i, c in enumerate(synth.clips(batch, n, seed=0, kind="mix")):
+        audio[i, 1:] = torch.from_numpy(c)
+    audio = audio.to(dev)
+    eng = NativeCodec(cfg, state, dev, with_generator=False, gemm="bf16")
+    T = eng.num_frames(n + 1)
+
+    def step():
+        return eng.vq_encode(eng.encode(eng.mel(audio)), want_pjt_in=False, want_fup=False, want_quantized=False)[0]
+
+    codes = step()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        codes = step()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    assert int(codes.min()) >= 0 and int(codes.max()) < cfg["quantizer"]["codebook_size"]
+    eng.profile(True)
+    eng.profile_reset()
+    step()
+    kern = eng.profile_read()
+    eng.profile(False)
+    name, rec = max(kern.items(), key=lambda kv: kv[1]["ms"])
+    prods = 2 if "prefilter_b" in name else 1
+    ach = rec["flops"] / (rec["ms"] * 1e-3) / 1e12
+    flops = C3_MFLOP_PER_FRAME * 1e6 * batch * T
+    out = {"workload": f"C3: encoder + GRFVQ token extraction, {batch} x 10 s, bf16 (enable_bfloat16), codes only",
+           "value": round(batch * n / (ms * 1e-3), 1), "unit": "samples/s", "ms_per_step": round(ms, 3),
+           "steps": steps, "warmup": 1, "tflops_algorithmic": round(flops / (ms * 1e-3) / 1e12, 1),
+           "frac_of_bf16_dense": round(flops / (ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4),
+           "dominant_kernel": {"kernel": name, "achieved": round(ach, 1), "unit": "TFLOP/s",
+                               "frac_of_bf16_dense": round(ach / BF16_MFMA_PEAK_TFLOPS, 4),
+                               "products_per_flop": prods,
+                               "frac_of_product_ceiling": round(ach * prods / BF16_MFMA_PEAK_TFLOPS, 4),
+                               "avg_launch_ms": round(rec["ms"] / rec["launches"], 4),
+                               "share_of_device_time": round(rec["ms"] / sum(v["ms"] for v in kern.values()), 4)}}
+    del eng
+    torch.cuda.empty_cache()
+    return out
+
+
+def c5_record(eng, hops: int = 100, warmup: int = 10, split_k: int = 16):
+    """BASELINE configs[4] (C5): B = 1, 1 s hops, each hop's encode -> decode one hipGraph replay
+    (streaming.GraphedHop) in the split-K latency mode; HIP events around each replay."""
+    from distilcodec_nabeel_amd.streaming import GraphedHop
+
+    n = SR
+    stream = np.concatenate(synth.clips(1, n * (hops + warmup), seed=3, kind="speech"))
+    chunks = torch.from_numpy(stream.reshape(-1, 1, n).astype(np.float32)).to(eng.device)
+    eng.set_split_k(split_k)
+    try:
+        hop = GraphedHop(eng, n)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(hops)]
+        for i in range(warmup):
+            hop(chunks[i])
+        torch.cuda.synchronize(eng.device)
+        for i in range(hops):
+            ev[i][0].record()
+            hop(chunks[warmup + i])
+            ev[i][1].record()
+        torch.cuda.synchronize(eng.device)
+        ms = np.array([a.elapsed_time(b) for a, b in ev])
+        del hop
+    finally:
+        eng.set_split_k(0)
+    return {"workload": "C5: streaming encode->decode, 1 s hops (24000 samples, B = 1), one hipGraph replay per hop, "
+                        f"split-K latency mode (<= {split_k} slices)",
+            "hops": hops, "warmup": warmup, "p50_ms": round(float(np.percentile(ms, 50)), 4),
+            "p99_ms": round(float(np.percentile(ms, 99)), 4), "mean_ms": round(float(ms.mean()), 4),
+            "real_time_factor_p99": round(float(np.percentile(ms, 99)) / 1000.0, 5)}
+
+
+def codes_vs_oracle(eng, runner, cfg, state):
+    """Clip 0 of the timed C2 batch (full 10 s) against the CPU oracle (oracle/reference_cpu.py, the
+    reference's algorithm on PyTorch-CPU): codes exact on every decisive frame (fp64 relative top-2
+    gap > 1e-4, computed with torch fp64 on the GPU), the raw exact-match rate, and the waveform SNR
+    (of the reference's codes decoded on the GPU when a non-decisive code differs)."""
+    from oracle import reference_cpu as R
+
+    torch.set_num_threads(_host_threads())
+    audio = runner.audio[:1].cpu()
+    t0 = time.perf_counter()
+    ref = R.encode_decode(audio, state, cfg)
+    t_ref = time.perf_counter() - t0
+    rc = ref["codes"][0, :, :, 0].numpy()
+    gc = runner.codes[:1].cpu().numpy().astype(np.int64)
+    x = ref["x_pjt_in"].reshape(-1, ref["x_pjt_in"].shape[-1]).to(eng.device, torch.float64)
+    E = R.codebook(state["quantizer"]).to(eng.device, torch.float64)
+    d = (x ** 2).sum(1)[:, None] + (E ** 2).sum(1)[None, :] - 2.0 * x @ E.T
+    v, _ = torch.topk(d, 2, dim=1, largest=False)
+    decisive = (((v[:, 1] - v[:, 0]) / v[:, 0]) > 1e-4).cpu().numpy().reshape(rc.shape)
+    del x, E, d
+    same = np.array_equal(gc, rc)
+    wav = runner.wav[:1] if same else eng.generate(eng.vq_decode(torch.from_numpy(rc).to(torch.int32)))
+    w, r = wav.double().cpu().numpy().reshape(-1), ref["wav"][:, 0].double().numpy().reshape(-1)
+    snr = 10 * np.log10((r ** 2).sum() / max(((w - r) ** 2).sum(), 1e-300))
+    return {"clip": "clip 0 of the timed C2 batch (10 s), oracle/reference_cpu.py fp32 on the host CPU",
+            "frames": int(gc.size), "decisive_frames": int(decisive.sum()),
+            "decisive_exact": bool(np.array_equal(gc[decisive], rc[decisive])),
+            "match_rate": round(float((gc == rc).mean()), 6),
+            "waveform_snr_db": round(float(snr), 2),
+            "waveform_of": "the GPU's own codes" if same else "the reference's codes decoded on the GPU (a non-decisive code differs)",
+            "oracle_seconds": round(t_ref, 2)}
+
+
 def make_runner(eng, workload: str, rank: int, world: int, seed: int = 0):
     per_gpu, longest, shortest = WORKLOADS[workload]
     n_total = per_gpu * world
@@ -169,6 +291,8 @@ def roofline(prof: dict, steps: int):
     peak = X6_PEAK_TFLOPS if "x6" in name else FP32_MFMA_PEAK_TFLOPS
     return {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": round(peak, 1),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic_for(name),
+            "traffic_source": "committed PMC figure (profiles/pmc_latest.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                              "passes over bench.py, 2*FETCH + WRITE per launch), not measured in this run",
             "peak_basis": ("bf16 dense MFMA 2500 TF / 6 bf16 products per fp32 product" if "x6" in name
                            else "fp32 MFMA v_mfma_f32_32x32x2_f32"),
             "launches_per_step": rec["launches"] // steps, "avg_launch_ms": round(avg_ms, 4),
@@ -182,7 +306,10 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", choices=sorted(WORKLOADS), default="c2")
-    ap.add_argument("--no-c4", action="store_true", help="skip the extra C4 pass at N > 1")
+    ap.add_argument("--no-c4", action="store_true", help="skip the extra C4 pass")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 token-extraction sub-record (N = 1)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming-hop sub-record (N = 1)")
+    ap.add_argument("--no-oracle-codes", action="store_true", help="skip the codes_vs_oracle check (N = 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-f32", action="store_true", help="skip the IEEE fp32-MFMA comparison pass at N = 1")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch HIP-event roofline timing")
@@ -207,20 +334,31 @@ def main():
     ms_step = dt / args.steps * 1e3
     value = samples / (dt / args.steps)
     padded = n_total * (runner.audio.shape[1] - 1)
+    frames = runner.frames
     roof = roofline(prof, args.steps)
     if roof and rank == 0 and os.environ.get("DCX_BENCH_KERNELS"):
         with open(os.environ["DCX_BENCH_KERNELS"], "w") as f:
             json.dump({"steps": args.steps, "kernels": prof}, f, indent=1)
 
+    oracle_codes = None
+    if world == 1 and args.config == "c2" and not args.no_oracle_codes:
+        oracle_codes = codes_vs_oracle(eng, runner, cfg, state)
+
     c4 = None
-    if world > 1 and args.config == "c2" and not args.no_c4:
+    if args.config == "c2" and not args.no_c4:
         r4, s4, n4 = make_runner(eng, "c4", rank, world)
-        k4 = min(args.steps, 3)
+        k4 = min(args.steps, 3 if world > 1 else 2)
         dt4, _ = run_timed(r4, k4, 1, world, dev)
         c4 = {"workload": f"C4: {n4} ragged clips (9-10 s, speech+music), {n4 // world} per GPU, padded to the global max",
-              "value": round(s4 / (dt4 / k4), 1), "unit": "samples/s", "ms_per_step": round(dt4 / k4 * 1e3, 3),
-              "steps": k4, "warmup": 1, "global_batch": n4}
+              "value": round(s4 / (dt4 / k4), 1), "unit": "samples/s (real, unpadded)",
+              "ms_per_step": round(dt4 / k4 * 1e3, 3), "steps": k4, "warmup": 1, "global_batch": n4,
+              "n_gpus": world}
         del r4
+        torch.cuda.empty_cache()
+
+    c5 = None
+    if world == 1 and args.config == "c2" and args.gemm == "x6" and not args.no_c5:
+        c5 = c5_record(eng)
 
     f32 = None
     if world == 1 and args.gemm == "x6" and not args.no_f32:
@@ -231,6 +369,13 @@ def main():
         f32 = {"value": round(samples / (dtf / kf), 1), "unit": "samples/s", "ms_per_step": round(dtf / kf * 1e3, 3),
                "steps": kf, "arith": "IEEE fp32 MFMA (v_mfma_f32_32x32x2_f32), same workload",
                "tflops": round(samples / 256 * MFLOP_PER_FRAME * 1e6 / (dtf / kf) / 1e12, 1)}
+
+    c3 = None
+    if world == 1 and args.config == "c2" and not args.no_c3:
+        del runner
+        eng._ws = None  # the C2 / C4 workspace is not needed by the token-extraction handle
+        torch.cuda.empty_cache()
+        c3 = c3_record(cfg, state, dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -259,12 +404,15 @@ def main():
                       "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
             "data": "synthetic (speech/music-like 24 kHz clips; seeded synthetic weights, no checkpoint offline)",
             "config": {"workload": workload, "global_batch": n_total, "clip_samples_max": longest,
-                       "frames_per_clip": runner.frames, "parallelism": f"clip-sharded x{world}, codes all_gather",
+                       "frames_per_clip": frames, "parallelism": f"clip-sharded x{world}, codes all_gather",
                        "padded_samples_per_s": round(padded / (dt / args.steps), 1)},
             "tflops_algorithmic": round(padded / 256 * MFLOP_PER_FRAME * 1e6 / (dt / args.steps) / 1e12, 1),
             "roofline": roof,
             "f32_ieee": f32,
+            "codes_vs_oracle": oracle_codes,
             "c4": c4,
+            "c3": c3,
+            "c5": c5,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

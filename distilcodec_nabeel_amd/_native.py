@@ -26,6 +26,7 @@ DCX_ERR_STATE = -3
 DCX_ERR_HIP = -4
 DCX_ERR_OOM = -5
 DCX_ERR_WORKSPACE = -6
+DCX_ERR_UNSUPPORTED = -7
 DCX_GEMM_F32 = 0
 DCX_GEMM_X6 = 1
 DCX_GEMM_BF16 = 2
@@ -75,6 +76,7 @@ SIGNATURES = {
     "dcx_num_frames": (_I64, [_P, _I64]),
     "dcx_workspace_size": (_SZ, [_P, _I32, _I64]),
     "dcx_mel": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _SZ, _P]),
+    "dcx_mel_linear": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _SZ, _P]),
     "dcx_encode": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _SZ, _P]),
     "dcx_vq_encode": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
     "dcx_vq_decode": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _SZ, _P]),
@@ -85,6 +87,8 @@ SIGNATURES = {
     "dcx_mp3_decode": (ctypes.c_int, [_P, _SZ, _P, _I64]),
     "dcx_mp3_last_error": (ctypes.c_char_p, []),
     "dcx_mp3_stats": (ctypes.c_int, [ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
+    "dcx_mp3_junk_bytes": (_I64, []),
+    "dcx_mp3_bad_frames": (_I64, []),
     "dcx_resample_poly": (ctypes.c_int, [_P, _I32, _I64, _I64, _P, _I32, _I32, _I32, _I64, _P, _I64, _I64, _P]),
     "dcx_set_gemm_mode": (ctypes.c_int, [_P, _I32]),
     "dcx_get_gemm_mode": (_I32, [_P]),
@@ -92,6 +96,8 @@ SIGNATURES = {
     "dcx_conv_create": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, ctypes.POINTER(_P)]),
     "dcx_conv_forward": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, _P, _P, _P, _I32, _P]),
     "dcx_conv_destroy": (None, [_P]),
+    "dcx_module_workspace_size": (_SZ, [_P, ctypes.c_char_p, _I32, _I64]),
+    "dcx_module_forward": (ctypes.c_int, [_P, ctypes.c_char_p, _P, _I32, _I64, _P, _P, _SZ, _P]),
     "dcx_vq_rescore_stats": (ctypes.c_int, [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I32]),
     "dcx_profile_enable": (ctypes.c_int, [_P, _I32]),
     "dcx_profile_reset": (ctypes.c_int, [_P]),

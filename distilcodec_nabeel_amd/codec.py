@@ -67,15 +67,21 @@ class _Part:
 
 
 class SpecTransform(_Part):
-    """LogMelSpectrogram (mel_spec.py:60-122): (B, N) / (B, 1, N) audio -> (B, n_mels, T)."""
+    """LogMelSpectrogram.forward (mel_spec.py:109-122): (B, N) / (B, 1, N) audio -> (B, n_mels, T).
+
+    `sample_rate` other than the model rate resamples first with torchaudio's default
+    `F.resample` (sinc_interp_hann, lowpass width 6, rolloff 0.99; mel_spec.py:112-113), on the GPU
+    (`resample.resample_sinc_hann`).  `return_linear=True` also returns the log-compressed linear
+    spectrogram (B, n_fft/2 + 1, T) (mel_spec.py:119-120)."""
 
     def __call__(self, x: torch.Tensor, return_linear: bool = False, sample_rate: int = None):
-        if return_linear:
-            raise NotImplementedError("return_linear is a training-side option")
         if sample_rate is not None and sample_rate != self._codec.spec_config.sampling_rate:
-            raise ValueError("resampling is not implemented on the native path")
+            x = resample.resample_sinc_hann(x, int(sample_rate), self._codec.spec_config.sampling_rate, self._eng.device)
         if x.ndim == 3:
             x = x.squeeze(1)
+        if return_linear:
+            mel, lin = self._eng.mel(x, linear=True)
+            return _cf(mel), _cf(lin)
         return _cf(self._eng.mel(x))
 
 
@@ -271,12 +277,19 @@ class DistilCodec:
         Like the reference (:155-160), ANY failure to read a file (missing, not audio, corrupt)
         substitutes 1 s of N(0,1)*0.05 noise.  Resampling of another rate (librosa.load(sr=24000))
         runs on the GPU outside that fallback, so a missing GPU still fails loudly.  The
-        reference's sample-rate ValueError (:161-163) cannot trigger after resampling; it is kept."""
+        reference's sample-rate ValueError (:161-163) cannot trigger after resampling; it is kept.
+        One exception is not a read failure: a valid MP3 stream in a format the host decoder lacks
+        (`mp3.Mp3Unsupported`: MPEG-2/2.5, Layer I/II, free format, intensity stereo) would decode in
+        the reference's librosa, so it is raised instead of being replaced by noise."""
+        from .mp3 import Mp3Unsupported
+
         audio_list = []
         sr_target = self.spec_config.sampling_rate
         for p in audio_pathes:
             try:
                 audio, sampling_rate = audio_io.load_audio_mono(p)
+            except Mp3Unsupported:
+                raise
             except Exception:
                 print(f"Error on audio: {p}")
                 audio = (np.random.normal(size=(sr_target,)) * 0.05).astype(np.float32)

@@ -8,6 +8,7 @@
 //   generate generators.py:118-147, convnext_utils.py:106-113,137-138
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -116,9 +117,11 @@ struct dcx_codec {
   // DCX_NO_COMPACT=1 at dcx_create keeps the planes layout (A/B comparisons, same bits)
   bool compact = true;
   // split-K latency mode (dcx_set_split_k): at most split_k K-slices per few-tile x6 conv; the
-  // partial sums live in the first kSplitScratch bytes of each stage call's workspace (split_buf)
+  // partial sums live in the first kSplitScratch bytes of each stage call's workspace.  split_buf
+  // points there only for the duration of one stage call (CallScope), which `busy` makes exclusive.
   int split_k = 0;
   float* split_buf = nullptr;
+  std::atomic<int> busy{0};
 
   ConvW conv_pre;
   ConvW ups[8];
@@ -765,7 +768,8 @@ int run_ln(dcx_codec* h, const LnW& l, const float* x, Act y, long long rows, hi
 }
 
 // ---------------- stage bodies (dry=true only sizes the workspace) ----------------
-int stage_mel(dcx_codec* h, const float* audio, int B, int64_t n, Act mel, Bump& ws, hipStream_t s) {
+int stage_mel(dcx_codec* h, const float* audio, int B, int64_t n, Act mel, Bump& ws, hipStream_t s,
+              float* loglin = nullptr) {
   const dcx_config& c = h->cfg;
   const int T = (int)frames_of(c, n);
   const int rows = T + c.n_fft / c.hop - 1;
@@ -783,7 +787,7 @@ int stage_mel(dcx_codec* h, const float* audio, int B, int64_t n, Act mel, Bump&
   RUN(run_conv(h, h->dft, cc, s));
   const int nbins = c.n_fft / 2 + 1;
   LAUNCH(h, s, "spec_mag", 4.0 * B * T * nbins, 4.0 * B * T * (h->dft.cout + h->melfb.cin),
-         dcx::launch_spec_mag(spec, mag.f, mag.p, (long long)B * T, nbins, h->melfb.cin, s));
+         dcx::launch_spec_mag(spec, mag.f, mag.p, loglin, (long long)B * T, nbins, h->melfb.cin, s));
   ConvCall cm = pointwise(mag, (long long)B * T);
   cm.exact = true;
   cm.out_to(mel);
@@ -818,6 +822,44 @@ int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipSt
     for (auto& bw : h->blocks[i]) RUN(run_block(h, bw, xb, nullptr, B, T, ln, hid, s));
   }
   RUN(run_ln(h, h->enc_norm, xb, feat, M, s));
+  return DCX_OK;
+}
+
+// The nearest-code search of DownsampleGRVQ (vector_quantize_pytorch.py:41-45, 496-506; first index on
+// ties) on x_pjt_in P (fp32 [M][CD]) and, in x6 / bf16 mode, P6 in the prefilter's layout xl (0 planes,
+// 1 compact bf16, 2 hm): |x|^2, the certified prefilter and the fp64 rescore (x6 / bf16), or the exact
+// fp32 distance GEMM and its reduce (fp32 mode).  pv / pi / pv2: [M][ntiles] scratch, x2: [M].
+int run_vq_search(dcx_codec* h, const float* P, const unsigned short* P6, int xl, long long M, float* x2, float* pv,
+                  int* pi, float* pv2, int ntiles, int32_t* codes, hipStream_t s) {
+  const dcx_config& c = h->cfg;
+  const int CD = c.codebook_dim, NC = c.codebook_size;
+  const bool x6 = x6_mode(h);
+  const bool p6c = xl == 1, p6hm = xl == 2;
+  LAUNCH(h, s, "row_sqnorm", 2.0 * M * CD, 4.0 * M * CD, dcx::launch_row_sqnorm(P, M, CD, x2, s));
+  {
+    ConvParams p{};
+    p.x = P; p.x6 = P6; p.w = h->codebook; p.w6 = x6 ? h->codebook6 : nullptr;
+    p.Cin = CD; p.Cout = NC; p.ldx = CD; p.taps = 1; p.in_step = 1; p.out_mul = 1;
+    p.x2 = x2; p.e2 = h->e2; p.part_val = pv; p.part_idx = pi; p.part_val2 = pv2;
+    p.x_compact = p6c ? 1 : p6hm ? 2 : 0;
+    p.wc = p6c || p6hm ? h->codebook_bk : nullptr;
+    ProfScope ps(h, s);
+    const char* kname = "vq";
+    if (x6) {
+      // bf16 mode rounds x_pjt_in to bf16 in the project_in epilogue (round_bf16)
+      HIPCHK(h, dcx::launch_vq_prefilter(p, (int)M, h->gemm_mode == DCX_GEMM_BF16, s, &kname));
+      ps.done(kname, 2.0 * M * NC * CD, 4.0 * ((double)M * CD + (double)NC * CD));
+    } else {
+      HIPCHK(h, dcx::launch_vq_argmin(p, (int)M, s, &kname));
+      ps.done(kname, 2.0 * M * NC * CD, 4.0 * ((double)M * CD + (double)NC * CD));
+    }
+  }
+  if (x6)
+    LAUNCH(h, s, "vq_rescore", 0, 12.0 * M * ntiles + 4.0 * M,
+           dcx::launch_vq_rescore(pv, pi, pv2, M, ntiles, NC / ntiles, P, x2, CD, h->codebook, h->emax, h->e2max,
+                                  dcx::kVqPrefilterBound, codes, h->vq_stats, s));
+  else
+    LAUNCH(h, s, "vq_reduce", 0, 8.0 * M * ntiles, dcx::launch_vq_reduce(pv, pi, (int)M, ntiles, codes, s));
   return DCX_OK;
 }
 
@@ -858,38 +900,14 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   cp.y6 = P6;
   cp.y6c = p6c ? 1 : p6hm ? 2 : 0;
   RUN(run_conv(h, h->vq_pin, cp, s));
-  LAUNCH(h, s, "row_sqnorm", 2.0 * M * CD, 4.0 * M * CD, dcx::launch_row_sqnorm(P, M, CD, x2, s));
-  {
-    ConvParams p{};
-    p.x = P; p.x6 = P6; p.w = h->codebook; p.w6 = x6 ? h->codebook6 : nullptr;
-    p.Cin = CD; p.Cout = NC; p.ldx = CD; p.taps = 1; p.in_step = 1; p.out_mul = 1;
-    p.x2 = x2; p.e2 = h->e2; p.part_val = pv; p.part_idx = pi; p.part_val2 = pv2;
-    p.x_compact = p6c ? 1 : p6hm ? 2 : 0;
-    p.wc = p6c || p6hm ? h->codebook_bk : nullptr;
-    ProfScope ps(h, s);
-    const char* kname = "vq";
-    if (x6) {
-      // bf16 mode rounds x_pjt_in to bf16 in the project_in epilogue (round_bf16)
-      HIPCHK(h, dcx::launch_vq_prefilter(p, (int)M, h->gemm_mode == DCX_GEMM_BF16, s, &kname));
-      ps.done(kname, 2.0 * M * NC * CD, 4.0 * ((double)M * CD + (double)NC * CD));
-    } else {
-      HIPCHK(h, dcx::launch_vq_argmin(p, (int)M, s, &kname));
-      ps.done(kname, 2.0 * M * NC * CD, 4.0 * ((double)M * CD + (double)NC * CD));
-    }
-  }
-  if (x6)
-    LAUNCH(h, s, "vq_rescore", 0, 12.0 * M * ntiles + 4.0 * M,
-           dcx::launch_vq_rescore(pv, pi, pv2, M, ntiles, NC / ntiles, P, x2, CD, h->codebook, h->emax, h->e2max,
-                                  dcx::kVqPrefilterBound, codes, h->vq_stats, s));
-  else
-    LAUNCH(h, s, "vq_reduce", 0, 8.0 * M * ntiles, dcx::launch_vq_reduce(pv, pi, (int)M, ntiles, codes, s));
-  if (fup) LAUNCH(h, s, "gather_rows", 0, 8.0 * M * CD, dcx::launch_gather_rows(h->codebook, NC, codes, M, CD, fup, nullptr, s));
+  RUN(run_vq_search(h, P, P6, p6c ? 1 : p6hm ? 2 : 0, M, x2, pv, pi, pv2, ntiles, codes, s));
+  if (fup) LAUNCH(h, s, "gather_rows", 0, 8.0 * M * CD, dcx::launch_gather_rows(h->codebook, NC, codes, M, CD, fup, nullptr, -1, s));
   if (quant) {
     if (x6)
       LAUNCH(h, s, "gather_rows", 0, 12.0 * M * D,
-             dcx::launch_gather_rows((const float*)h->ptable6, NC, codes, M, D * 3 / 2, (float*)zd.p, nullptr, s));
+             dcx::launch_gather_rows((const float*)h->ptable6, NC, codes, M, D * 3 / 2, (float*)zd.p, nullptr, NC, s));
     else
-      LAUNCH(h, s, "gather_rows", 0, 8.0 * M * D, dcx::launch_gather_rows(h->ptable, NC, codes, M, D, zd.f, nullptr, s));
+      LAUNCH(h, s, "gather_rows", 0, 8.0 * M * D, dcx::launch_gather_rows(h->ptable, NC, codes, M, D, zd.f, nullptr, NC, s));
     ConvCall cu = pointwise(zd, M);
     cu.y = quant;
     RUN(run_conv(h, h->vq_up, cu, s));
@@ -912,10 +930,10 @@ int stage_vq_decode(dcx_codec* h, const int32_t* codes, int B, int T, Act z, int
   if (x6_mode(h))
     LAUNCH(h, s, "gather_rows", 0, 12.0 * M * D,
            dcx::launch_gather_rows((const float*)h->ptable6, c.codebook_size, codes, M, D * 3 / 2, (float*)zd.p,
-                                   n_invalid, s));
+                                   n_invalid, c.codebook_size, s));
   else
     LAUNCH(h, s, "gather_rows", 0, 8.0 * M * D,
-           dcx::launch_gather_rows(h->ptable, c.codebook_size, codes, M, D, zd.f, n_invalid, s));
+           dcx::launch_gather_rows(h->ptable, c.codebook_size, codes, M, D, zd.f, n_invalid, c.codebook_size, s));
   ConvCall cu = pointwise(zd, M);
   cu.y = z.f;
   RUN(run_conv(h, h->vq_up, cu, s));
@@ -939,6 +957,111 @@ bool res_pair_ok(const dcx_codec* h, int stage) {
           return false;
       }
   return true;
+}
+
+// Buffers of one generator stage's ParallelBlock (run_parallel_block).
+struct PBlockBufs {
+  float* X = nullptr;                // ConvT output: the ResBlocks' input (fp32)
+  Act XS;                            // silu(X) in the c1 convs' input form (unused when silu is applied on load)
+  float* R[dcx::kMaxGroup] = {};     // ResBlock states (fp32)
+  Act RS[dcx::kMaxGroup];            // silu(R), c1 input form
+  Act Tb[dcx::kMaxGroup];            // silu(c1 output) buffers as allocated
+  Act Tb_in[dcx::kMaxGroup];         // the same in the c2 convs' input form
+  float* Mx = nullptr;               // mean accumulator; silu(mean) in fp32 when `last`
+  Act next;                          // silu(mean) in the next ConvT's input form (not `last`)
+  bool last = false;
+};
+
+// ParralelBlock.forward (convnext_utils.py:137-138) of generator stage i: three ResBlock1
+// (convnext_utils.py:106-113) on X, their mean, and the SiLU that follows it in the generator
+// (generators.py:125 / :141), written to b.Mx as fp32 (b.last) or to b.next.  The C = 32 / 64
+// stages run as fused pairs (conv_res_pair), the others as grouped per-conv launches.
+int run_parallel_block(dcx_codec* h, int i, int B, int Lo, const PBlockBufs& b, hipStream_t s) {
+  const dcx_config& c = h->cfg;
+  constexpr int NR = dcx::kMaxGroup;
+  const ConvW& rconv = h->res[i][0][0][0];  // every ResBlock conv of the stage has Cin = Cout = Co
+  const int Co = rconv.cout;
+  const bool silu_on_load = x6_mode(h) && f32_input_ok(rconv);
+  if (silu_on_load && res_pair_ok(h, i)) {
+    // fused pairs: X -> R[rb] -> Tb[rb] (as fp32) -> silu(ParallelBlock mean)
+    float* Ra[NR];
+    float* Rb[NR];
+    for (int rb = 0; rb < c.n_res; ++rb) {
+      Ra[rb] = b.R[rb];
+      Rb[rb] = b.Tb[rb].f ? b.Tb[rb].f : reinterpret_cast<float*>(b.Tb[rb].p);
+    }
+    float* out = b.last ? b.Mx : b.next.f;
+    for (int ci = 0; ci < 3; ++ci) {
+      dcx::ResPairParams rp{};
+      double fl = 0, by = 0;
+      for (int rb = 0; rb < c.n_res; ++rb) {
+        const ConvW& w1 = h->res[i][rb][ci][0];
+        const ConvW& w2 = h->res[i][rb][ci][1];
+        rp.src[rb] = ci == 0 ? b.X : (ci == 1 ? Ra[rb] : Rb[rb]);
+        rp.dst[rb] = ci == 0 ? Ra[rb] : (ci == 1 ? Rb[rb] : nullptr);
+        rp.w1[rb] = w1.w6;
+        rp.w2[rb] = w2.w6;
+        rp.b1[rb] = w1.b;
+        rp.b2[rb] = w2.b;
+        rp.taps[rb] = w1.taps;
+        rp.dil[rb] = w1.in_step;
+        ConvCall cc = framed(Act{b.X, nullptr}, B, Lo, Co);
+        fl += conv_flops(w1, cc) + conv_flops(w2, cc);
+        by += 8.0 * B * Lo * Co;
+      }
+      rp.nmem = c.n_res;
+      rp.mean_out = ci == 2 ? out : nullptr;
+      rp.bstride = (long long)Lo * Co;
+      rp.L = Lo;
+      rp.batch = B;
+      rp.C = Co;
+      ProfScope ps(h, s);
+      const char* kname = "conv_res_pair";
+      HIPCHK(h, dcx::launch_res_pair(rp, s, &kname));
+      ps.done(kname, fl, by);
+    }
+    return DCX_OK;
+  }
+  for (int ci = 0; ci < 3; ++ci) {
+    const ConvW* w1[NR];
+    ConvCall c1[NR];
+    for (int rb = 0; rb < c.n_res; ++rb) {  // c1 of every ResBlock: one grouped launch
+      const Act src = silu_on_load ? Act{ci == 0 ? b.X : b.R[rb], nullptr} : (ci == 0 ? b.XS : b.RS[rb]);
+      c1[rb] = framed(src, B, Lo, Co);
+      c1[rb].silu_in = silu_on_load;
+      c1[rb].silu_to(b.Tb_in[rb]);
+      w1[rb] = &h->res[i][rb][ci][0];
+    }
+    RUN(run_conv_group(h, w1, c1, c.n_res, s));
+    if (ci < 2) {  // c2 of every ResBlock: grouped; residual X (first pair) or the block's state
+      const ConvW* w2[NR];
+      ConvCall c2[NR];
+      for (int rb = 0; rb < c.n_res; ++rb) {
+        c2[rb] = framed(b.Tb_in[rb], B, Lo, Co);
+        c2[rb].epi = dcx::EPI_RES;
+        c2[rb].res = ci == 0 ? b.X : b.R[rb];
+        c2[rb].y = b.R[rb];
+        if (!silu_on_load) c2[rb].silu_to(b.RS[rb]);
+        w2[rb] = &h->res[i][rb][ci][1];
+      }
+      RUN(run_conv_group(h, w2, c2, c.n_res, s));
+    } else {  // last pair: ParallelBlock mean folded into the epilogues, in ResBlock order
+      for (int rb = 0; rb < c.n_res; ++rb) {
+        ConvCall cc = framed(b.Tb_in[rb], B, Lo, Co);
+        cc.epi = dcx::EPI_RES;
+        cc.res = b.R[rb];
+        cc.macc = b.Mx;
+        cc.mean = rb == 0 ? dcx::MEAN_FIRST : (rb == c.n_res - 1 ? dcx::MEAN_LAST : dcx::MEAN_MID);
+        if (rb == c.n_res - 1) {
+          // silu(mean): input of ups[i+1], or (fp32, in place) of conv_post
+          if (b.last) cc.y2 = b.Mx;
+          else cc.silu_to(b.next);  // input of the next ConvT
+        }
+        RUN(run_conv(h, h->res[i][rb][ci][1], cc, s));
+      }
+    }
+  }
+  return DCX_OK;
 }
 
 int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hipStream_t s) {
@@ -993,88 +1116,19 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
       if (!silu_on_load) cc.silu_to(XS_i);
       RUN(run_conv(h, up, cc, s));
     }
-    const bool last_stage = i == c.n_ups - 1;
-    if (silu_on_load && res_pair_ok(h, i)) {
-      // fused pairs: X -> R[rb] -> Tb[rb] (as fp32) -> silu(ParallelBlock mean)
-      float* Ra[NR];
-      float* Rb[NR];
-      for (int rb = 0; rb < c.n_res; ++rb) {
-        Ra[rb] = R[rb];
-        Rb[rb] = Tb[rb].f ? Tb[rb].f : reinterpret_cast<float*>(Tb[rb].p);
-      }
-      float* out = last_stage ? Mx : in_form(S, h->ups[i + 1]).f;
-      for (int ci = 0; ci < 3; ++ci) {
-        dcx::ResPairParams rp{};
-        double fl = 0, by = 0;
-        for (int rb = 0; rb < c.n_res; ++rb) {
-          const ConvW& w1 = h->res[i][rb][ci][0];
-          const ConvW& w2 = h->res[i][rb][ci][1];
-          rp.src[rb] = ci == 0 ? X : (ci == 1 ? Ra[rb] : Rb[rb]);
-          rp.dst[rb] = ci == 0 ? Ra[rb] : (ci == 1 ? Rb[rb] : nullptr);
-          rp.w1[rb] = w1.w6;
-          rp.w2[rb] = w2.w6;
-          rp.b1[rb] = w1.b;
-          rp.b2[rb] = w2.b;
-          rp.taps[rb] = w1.taps;
-          rp.dil[rb] = w1.in_step;
-          ConvCall cc = framed(Act{X, nullptr}, B, Lo, Co);
-          fl += conv_flops(w1, cc) + conv_flops(w2, cc);
-          by += 8.0 * B * Lo * Co;
-        }
-        rp.nmem = c.n_res;
-        rp.mean_out = ci == 2 ? out : nullptr;
-        rp.bstride = (long long)Lo * Co;
-        rp.L = Lo;
-        rp.batch = B;
-        rp.C = Co;
-        ProfScope ps(h, s);
-        const char* kname = "conv_res_pair";
-        HIPCHK(h, dcx::launch_res_pair(rp, s, &kname));
-        ps.done(kname, fl, by);
-      }
-      C = Co;
-      L = Lo;
-      continue;
+    PBlockBufs pb;
+    pb.X = X;
+    pb.XS = XS_i;
+    for (int rb = 0; rb < c.n_res; ++rb) {
+      pb.R[rb] = R[rb];
+      pb.RS[rb] = RS_i[rb];
+      pb.Tb[rb] = Tb[rb];
+      pb.Tb_in[rb] = Tb_i[rb];
     }
-    for (int ci = 0; ci < 3; ++ci) {
-      const ConvW* w1[NR];
-      ConvCall c1[NR];
-      for (int rb = 0; rb < c.n_res; ++rb) {  // c1 of every ResBlock: one grouped launch
-        const Act src = silu_on_load ? Act{ci == 0 ? X : R[rb], nullptr} : (ci == 0 ? XS_i : RS_i[rb]);
-        c1[rb] = framed(src, B, Lo, Co);
-        c1[rb].silu_in = silu_on_load;
-        c1[rb].silu_to(Tb_i[rb]);
-        w1[rb] = &h->res[i][rb][ci][0];
-      }
-      RUN(run_conv_group(h, w1, c1, c.n_res, s));
-      if (ci < 2) {  // c2 of every ResBlock: grouped; residual X (first pair) or the block's state
-        const ConvW* w2[NR];
-        ConvCall c2[NR];
-        for (int rb = 0; rb < c.n_res; ++rb) {
-          c2[rb] = framed(Tb_i[rb], B, Lo, Co);
-          c2[rb].epi = dcx::EPI_RES;
-          c2[rb].res = ci == 0 ? X : R[rb];
-          c2[rb].y = R[rb];
-          if (!silu_on_load) c2[rb].silu_to(RS_i[rb]);
-          w2[rb] = &h->res[i][rb][ci][1];
-        }
-        RUN(run_conv_group(h, w2, c2, c.n_res, s));
-      } else {  // last pair: ParallelBlock mean folded into the epilogues, in ResBlock order
-        for (int rb = 0; rb < c.n_res; ++rb) {
-          ConvCall cc = framed(Tb_i[rb], B, Lo, Co);
-          cc.epi = dcx::EPI_RES;
-          cc.res = R[rb];
-          cc.macc = Mx;
-          cc.mean = rb == 0 ? dcx::MEAN_FIRST : (rb == c.n_res - 1 ? dcx::MEAN_LAST : dcx::MEAN_MID);
-          if (rb == c.n_res - 1) {
-            // silu(mean): input of ups[i+1], or (fp32, in place) of conv_post
-            if (last_stage) cc.y2 = Mx;
-            else cc.silu_to(in_form(S, h->ups[i + 1]));  // input of the next ConvT
-          }
-          RUN(run_conv(h, h->res[i][rb][ci][1], cc, s));
-        }
-      }
-    }
+    pb.Mx = Mx;
+    pb.last = i == c.n_ups - 1;
+    if (!pb.last) pb.next = in_form(S, h->ups[i + 1]);
+    RUN(run_parallel_block(h, i, B, Lo, pb, s));
     C = Co;
     L = Lo;
   }
@@ -1116,6 +1170,140 @@ int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int3
   return DCX_OK;
 }
 
+// ---------------- single reference modules (dcx_module_forward) ----------------
+// "<prefix>.%d[.%d]" matched exactly (the whole name consumed).
+bool match_idx(const std::string& m, const char* fmt, int* a, int* b = nullptr) {
+  int n = -1;
+  const int want = b ? 2 : 1;
+  const int got = b ? std::sscanf(m.c_str(), fmt, a, b, &n) : std::sscanf(m.c_str(), fmt, a, &n);
+  return got == want && n == (int)m.size();
+}
+
+// One module of the reference by its state-dict prefix, on the handle's packed weights and through
+// the same launches the stages use.  x / y: channels-last fp32 [B][L][C] (codes int32 [B][L] for
+// "quantizer.search").  See dcx_module_forward in the header for the list.
+int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int L, void* yv, Bump& ws, hipStream_t s) {
+  const dcx_config& c = h->cfg;
+  const long long M = (long long)B * L;
+  float* y = static_cast<float*>(yv);
+  int a = -1, b = -1;
+  // ConvNeXtBlock (convnext_utils.py:263-282)
+  const BlockW* blk = nullptr;
+  if (match_idx(m, "encoder.stages.%d.%d%n", &a, &b) && a >= 0 && a < 4 && b >= 0 && b < (int)h->blocks[a].size())
+    blk = &h->blocks[a][b];
+  else if (m == "quantizer.downsample.0.1") blk = &h->vq_down_blk;
+  else if (m == "quantizer.upsample.0.1") blk = &h->vq_up_blk;
+  if (blk) {
+    if (!blk->C) return fail(h, DCX_ERR_STATE, "module weights not finalized");
+    Act ln = conv_input(h, ws, (size_t)M * blk->C);
+    Act hid = conv_input(h, ws, (size_t)M * 4 * blk->C);
+    if (ws.dry) return DCX_OK;
+    if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    HIPCHK(h, hipMemcpyAsync(y, x, sizeof(float) * M * blk->C, hipMemcpyDeviceToDevice, s));
+    return run_block(h, *blk, y, nullptr, B, L, ln, hid, s);
+  }
+  // channels-first LayerNorm (convnext_utils.py:186-213)
+  const LnW* lw = nullptr;
+  if (m == "encoder.downsample_layers.0.1") lw = &h->stem_ln;
+  else if (match_idx(m, "encoder.downsample_layers.%d.0%n", &a) && a >= 1 && a < 4) lw = &h->ds_ln[a];
+  else if (m == "encoder.norm") lw = &h->enc_norm;
+  if (lw) {
+    if (ws.dry) return DCX_OK;
+    return run_ln(h, *lw, x, Act{y, nullptr}, M, s);
+  }
+  // nearest-code search on x_pjt_in (EuclideanCodebook.forward, vector_quantize_pytorch.py:496-506)
+  if (m == "quantizer.search") {
+    if (!h->codebook) return fail(h, DCX_ERR_STATE, "module weights not finalized");
+    const int CD = c.codebook_dim, NC = c.codebook_size;
+    if (h->gemm_mode == DCX_GEMM_BF16) return fail(h, DCX_ERR_INVALID_ARG, "quantizer.search takes x6 or fp32 arithmetic");
+    const bool x6 = x6_mode(h);
+    const bool hm = x6 && h->compact && h->codebook_bk && dcx::vq_hm_takes(NC, CD, M);
+    const int ntiles = x6 ? dcx::vq_prefilter_ntiles(NC, CD, M, hm ? 2 : 0) : dcx::vq_argmin_ntiles(NC);
+    unsigned short* P6 = x6 ? ws.u16((size_t)M * CD * 3) : nullptr;
+    float* x2 = ws.f((size_t)M);
+    float* pv = ws.f((size_t)M * ntiles);
+    int* pi = ws.i((size_t)M * ntiles);
+    float* pv2 = x6 ? ws.f((size_t)M * ntiles) : nullptr;
+    if (ws.dry) return DCX_OK;
+    if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    if (x6) LAUNCH(h, s, "split_planes", 0, 10.0 * M * CD, dcx::launch_split_planes(x, P6, M, CD, hm ? 2 : 0, s));
+    return run_vq_search(h, x, P6, hm ? 2 : 0, M, x2, pv, pi, pv2, ntiles, static_cast<int32_t*>(yv), s);
+  }
+  if (!h->has_gen && m.rfind("generator.", 0) == 0) return fail(h, DCX_ERR_STATE, "generator weights were not finalized");
+  // ConvTranspose1d (generators.py:118-147, ups[i])
+  if (match_idx(m, "generator.ups.%d%n", &a) && a >= 0 && a < c.n_ups) {
+    const ConvW& up = h->ups[a];
+    CAct in(x, nullptr);
+    if (!(x6_mode(h) && f32_input_ok(up))) RUN(ensure_planes(h, in, M, up.cin, ws, s));
+    if (ws.dry) return DCX_OK;
+    if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    ConvCall cc = framed(in, B, L, up.cin);
+    cc.y = y;
+    return run_conv(h, up, cc, s);
+  }
+  auto in_form = [&](const Act& v, const ConvW& consumer) -> Act {
+    if (!x6_mode(h) || !f32_input_ok(consumer)) return v;
+    return Act{v.f ? v.f : reinterpret_cast<float*>(v.p), nullptr};
+  };
+  // ResBlock1 (convnext_utils.py:106-113), as per-conv launches of the production conv kernels
+  if (match_idx(m, "generator.resblocks.%d.blocks.%d%n", &a, &b) && a >= 0 && a < c.n_ups && b >= 0 && b < c.n_res) {
+    const ConvW& w0 = h->res[a][b][0][0];
+    const int C = w0.cout;
+    Act XS = conv_input(h, ws, (size_t)M * C);  // silu(state), the c1 input (unless silu on load)
+    Act Tb = conv_input(h, ws, (size_t)M * C);  // silu(c1 output)
+    if (ws.dry) return DCX_OK;
+    if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    const bool silu_on_load = x6_mode(h) && f32_input_ok(w0);
+    const Act XSi = in_form(XS, w0), Tbi = in_form(Tb, w0);
+    HIPCHK(h, hipMemcpyAsync(y, x, sizeof(float) * M * C, hipMemcpyDeviceToDevice, s));
+    if (!silu_on_load) LAUNCH(h, s, "silu_act", 0, 10.0 * M * C, dcx::launch_silu_act(y, XSi.f, XSi.p, M, C, s));
+    for (int ci = 0; ci < 3; ++ci) {
+      ConvCall c1 = framed(silu_on_load ? Act{y, nullptr} : XSi, B, L, C);
+      c1.silu_in = silu_on_load;
+      c1.silu_to(Tbi);
+      RUN(run_conv(h, h->res[a][b][ci][0], c1, s));
+      ConvCall c2 = framed(Tbi, B, L, C);
+      c2.epi = dcx::EPI_RES;
+      c2.res = y;
+      c2.y = y;
+      if (!silu_on_load && ci < 2) c2.silu_to(XSi);
+      RUN(run_conv(h, h->res[a][b][ci][1], c2, s));
+    }
+    return DCX_OK;
+  }
+  // ParralelBlock of stage i followed by the generator's SiLU: silu(mean of the ResBlock1s), fp32
+  if (match_idx(m, "generator.resblocks.%d%n", &a) && a >= 0 && a < c.n_ups) {
+    constexpr int NR = dcx::kMaxGroup;
+    const ConvW& w0 = h->res[a][0][0][0];
+    const int C = w0.cout;
+    const size_t per = (size_t)M * C;
+    float* X = ws.f(per);
+    Act XS = conv_input(h, ws, per);
+    PBlockBufs pb;
+    Act RS[NR];
+    for (int rb = 0; rb < c.n_res; ++rb) {
+      pb.R[rb] = ws.f(per);
+      RS[rb] = conv_input(h, ws, per);
+      pb.Tb[rb] = conv_input(h, ws, per);
+    }
+    if (ws.dry) return DCX_OK;
+    if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    const bool silu_on_load = x6_mode(h) && f32_input_ok(w0);
+    HIPCHK(h, hipMemcpyAsync(X, x, sizeof(float) * per, hipMemcpyDeviceToDevice, s));
+    pb.X = X;
+    pb.XS = in_form(XS, w0);
+    for (int rb = 0; rb < c.n_res; ++rb) {
+      pb.RS[rb] = in_form(RS[rb], w0);
+      pb.Tb_in[rb] = in_form(pb.Tb[rb], w0);
+    }
+    if (!silu_on_load) LAUNCH(h, s, "silu_act", 0, 10.0 * per, dcx::launch_silu_act(X, pb.XS.f, pb.XS.p, M, C, s));
+    pb.Mx = y;
+    pb.last = true;
+    return run_parallel_block(h, a, B, L, pb, s);
+  }
+  return fail(h, DCX_ERR_INVALID_ARG, "unknown module: " + m);
+}
+
 int check_ready(dcx_codec* h, bool need_gen) {
   if (!h) return DCX_ERR_INVALID_ARG;
   if (!h->finalized) return fail(h, DCX_ERR_STATE, "dcx_finalize has not been called");
@@ -1149,6 +1337,7 @@ const char* dcx_status_string(int st) {
     case DCX_ERR_HIP: return "HIP error";
     case DCX_ERR_OOM: return "out of device memory";
     case DCX_ERR_WORKSPACE: return "workspace too small";
+    case DCX_ERR_UNSUPPORTED: return "unsupported input format";
     default: return "unknown status";
   }
 }
@@ -1302,16 +1491,19 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
           return fail(h, DCX_ERR_HIP, "bf16 codebook repack failed");
       }
     }
-    // decode table: project_out applied to every code once, E * W_out^T + b_out
-    h->ptable = B.alloc((size_t)NC * D);
-    h->ptable6 = (unsigned short*)B.alloc((size_t)NC * D * 3 / 2);
+    // decode table: project_out applied to every code once, E * W_out^T + b_out.  Row NC holds
+    // project_out(0) = b_out, the row of the reference's masked code -1 (residual_vq.py:120-127:
+    // masked_fill(-1 -> 0), gather, then the gathered vector zeroed before project_out).
+    h->ptable = B.alloc((size_t)(NC + 1) * D);
+    h->ptable6 = (unsigned short*)B.alloc((size_t)(NC + 1) * D * 3 / 2);
     if (!B.bad() && !B.dry) {
       // built once with the fp32 MFMA path (the codebook is not held as activation planes)
       ConvCall cp = pointwise(CAct(h->codebook, nullptr), NC);
       cp.y = h->ptable;
       int rc = run_conv(h, pout, cp, 0, /*force_f32=*/true);
       if (rc != DCX_OK) return rc;
-      if (dcx::launch_split_planes(h->ptable, h->ptable6, NC, D, 0, 0) != hipSuccess ||
+      if (hipMemcpy(h->ptable + (size_t)NC * D, pout.b, sizeof(float) * D, hipMemcpyDeviceToDevice) != hipSuccess ||
+          dcx::launch_split_planes(h->ptable, h->ptable6, NC + 1, D, 0, 0) != hipSuccess ||
           hipDeviceSynchronize() != hipSuccess)
         return fail(h, DCX_ERR_HIP, "decode-table build failed");
     }
@@ -1379,10 +1571,31 @@ size_t dcx_workspace_size(const dcx_codec* h, int32_t batch, int64_t frames) {
   return need + 4096;
 }
 
+// One stage call on a handle.  A handle is not re-entrant (the header's contract): a second call
+// entering while one runs (another thread sharing the handle) is refused with DCX_ERR_STATE rather
+// than left to overwrite the first call's split-K scratch pointer.  split_buf is cleared on exit, so
+// no later call (or dcx_workspace_size's dry run) sees a pointer into another call's workspace.
+struct CallScope {
+  dcx_codec* h;
+  bool owner = false;
+  explicit CallScope(dcx_codec* hh) : h(hh) {
+    int expect = 0;
+    owner = h && h->busy.compare_exchange_strong(expect, 1);
+  }
+  ~CallScope() {
+    if (owner) {
+      h->split_buf = nullptr;
+      h->busy.store(0);
+    }
+  }
+};
+
 #define STAGE_PRE(need_gen)                                           \
   int rc_ = check_ready(h, need_gen);                                 \
   if (rc_ != DCX_OK) return rc_;                                      \
   if (batch <= 0) return fail(h, DCX_ERR_INVALID_ARG, "batch must be > 0"); \
+  CallScope scope_(h);                                                \
+  if (!scope_.owner) return fail(h, DCX_ERR_STATE, "handle in use by a concurrent call (serialise calls per handle)"); \
   hipStream_t s = (hipStream_t)stream;                                \
   Bump ws(workspace, ws_bytes, false);                                \
   h->split_buf = h->split_k > 1 ? (float*)ws.raw(kSplitScratch) : nullptr
@@ -1394,6 +1607,15 @@ int dcx_mel(dcx_codec* h, const float* audio, int32_t batch, int64_t n, float* m
   if (n <= (h->cfg.win - h->cfg.hop) / 2 || frames_of(h->cfg, n) < 1)
     return fail(h, DCX_ERR_INVALID_ARG, "clip too short for the reflect pad / one STFT frame");
   return stage_mel(h, audio, batch, n, Act{mel, nullptr}, ws, s);
+}
+
+int dcx_mel_linear(dcx_codec* h, const float* audio, int32_t batch, int64_t n, float* mel, float* log_linear,
+                   void* workspace, size_t ws_bytes, void* stream) {
+  STAGE_PRE(false);
+  if (!audio || !mel || !log_linear) return fail(h, DCX_ERR_INVALID_ARG, "null buffer");
+  if (n <= (h->cfg.win - h->cfg.hop) / 2 || frames_of(h->cfg, n) < 1)
+    return fail(h, DCX_ERR_INVALID_ARG, "clip too short for the reflect pad / one STFT frame");
+  return stage_mel(h, audio, batch, n, Act{mel, nullptr}, ws, s, log_linear);
 }
 
 int dcx_encode(dcx_codec* h, const float* mel, int32_t batch, int64_t frames, float* feat, void* workspace,
@@ -1431,6 +1653,20 @@ int dcx_encode_decode(dcx_codec* h, const float* audio, int32_t batch, int64_t n
   if (n <= (h->cfg.win - h->cfg.hop) / 2 || frames_of(h->cfg, n) < 1)
     return fail(h, DCX_ERR_INVALID_ARG, "clip too short for the reflect pad / one STFT frame");
   return stage_encode_decode(h, audio, batch, n, codes, wav, ws, s);
+}
+
+size_t dcx_module_workspace_size(const dcx_codec* h, const char* module, int32_t batch, int64_t rows) {
+  if (!h || !module || batch <= 0 || rows <= 0 || !h->finalized) return 0;
+  Bump d(nullptr, 0, true);
+  if (stage_module(const_cast<dcx_codec*>(h), module, nullptr, batch, (int)rows, nullptr, d, 0) != DCX_OK) return 0;
+  return d.off + 4096;
+}
+
+int dcx_module_forward(dcx_codec* h, const char* module, const float* x, int32_t batch, int64_t rows, void* y,
+                       void* workspace, size_t ws_bytes, void* stream) {
+  STAGE_PRE(false);
+  if (!module || !x || !y || rows <= 0 || rows > (1 << 30)) return fail(h, DCX_ERR_INVALID_ARG, "bad arguments");
+  return stage_module(h, module, x, batch, (int)rows, y, ws, s);
 }
 
 int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int64_t cols, void* stream) {

@@ -150,11 +150,12 @@ bool vq_bk_takes(int ncodes, int dim);
 bool vq_hm_takes(int ncodes, int dim, long long rows);
 hipError_t launch_frame_pad(const float* audio, float* frames, unsigned short* frames6, int batch, long long n, int rows,
                             int hop, int pad_left, hipStream_t s);
-hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, long long rows, int nbins, int ld_out,
-                           hipStream_t s);
+hipError_t launch_silu_act(const float* x, float* yf, unsigned short* y6, long long rows, int C, hipStream_t s);
+hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, float* loglin, long long rows, int nbins,
+                           int ld_out, hipStream_t s);
 hipError_t launch_split_planes(const float* x, unsigned short* y6, long long rows, int C, int compact, hipStream_t s);
 hipError_t launch_gather_rows(const float* table, int ntable, const int32_t* idx, long long rows, int width,
-                              float* out, int32_t* n_invalid, hipStream_t s);
+                              float* out, int32_t* n_invalid, int masked_row, hipStream_t s);
 hipError_t launch_conv_post_tanh(const float* x, const float* w, float bias, float* out, int batch, int L, int C,
                                  int k, hipStream_t s);
 hipError_t launch_transpose(const float* in, float* out, int batch, long long rows, long long cols, hipStream_t s);

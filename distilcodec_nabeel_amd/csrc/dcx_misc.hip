@@ -208,9 +208,10 @@ hipError_t launch_frame_pad(const float* audio, float* frames, unsigned short* f
 
 // |STFT| = sqrt(re^2 + im^2 + 1e-6) (mel_spec.py:54-55).  spec columns: [0, nbins) real part of
 // bins 0..nbins-1, [nbins, 2*nbins-2) imaginary part of bins 1..nbins-2 (bins 0 and n_fft/2 are
-// real for a real signal).  Output row padded with zeros to ld_out.
+// real for a real signal).  Output row padded with zeros to ld_out.  Optional loglin [rows][nbins]:
+// compress(linear) = log(clamp(|STFT|, 1e-5)), the second output of return_linear (mel_spec.py:119-120).
 __global__ void spec_mag_kernel(const float* __restrict__ spec, float* __restrict__ mag, unsigned short* __restrict__ mag6,
-                                long long rows, int nbins, int ld_out) {
+                                float* __restrict__ loglin, long long rows, int nbins, int ld_out) {
   const long long row = blockIdx.x;
   if (row >= rows) return;
   const int ld_in = 2 * nbins - 2;
@@ -224,6 +225,7 @@ __global__ void spec_mag_kernel(const float* __restrict__ spec, float* __restric
         const float re = spec[row * ld_in + k];
         const float im = (k > 0 && k < nbins - 1) ? spec[row * ld_in + nbins + k - 1] : 0.f;
         o[e] = sqrtf((re * re + im * im) + 1e-6f);
+        if (loglin) loglin[row * nbins + k] = logf(fmaxf(o[e], 1e-5f));
       }
     }
     if (mag) *reinterpret_cast<f32x4*>(mag + row * ld_out + k4) = f32x4{o[0], o[1], o[2], o[3]};
@@ -231,10 +233,35 @@ __global__ void spec_mag_kernel(const float* __restrict__ spec, float* __restric
   }
 }
 
-hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, long long rows, int nbins, int ld_out,
-                           hipStream_t s) {
-  if (ld_out % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(spec_mag_kernel, dim3((unsigned)rows), dim3(256), 0, s, spec, mag, mag6, rows, nbins, ld_out);
+hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, float* loglin, long long rows, int nbins,
+                           int ld_out, hipStream_t s) {
+  if (ld_out % 8 || ld_out < nbins) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(spec_mag_kernel, dim3((unsigned)rows), dim3(256), 0, s, spec, mag, mag6, loglin, rows, nbins, ld_out);
+  return hipGetLastError();
+}
+
+// silu(x) as fp32 and/or planes (dcx_module_forward's ResBlock / ParallelBlock entries: the
+// generator itself produces these in conv epilogues).  Same arithmetic as the epilogues' silu.
+__global__ void __launch_bounds__(256) silu_act_kernel(const float* __restrict__ x, float* __restrict__ yf,
+                                                        unsigned short* __restrict__ y6, long long rows, int C) {
+  const long long total4 = rows * C / 4;
+  for (long long i4 = (long long)blockIdx.x * 256 + threadIdx.x; i4 < total4; i4 += (long long)gridDim.x * 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + i4 * 4);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = v[e] * __builtin_amdgcn_rcpf(1.0f + __expf(-v[e]));
+    if (yf) *reinterpret_cast<f32x4*>(yf + i4 * 4) = f32x4{o[0], o[1], o[2], o[3]};
+    if (y6) store_planes4(y6, (i4 * 4) / C, C, (int)((i4 * 4) % C), o[0], o[1], o[2], o[3]);
+  }
+}
+
+hipError_t launch_silu_act(const float* x, float* yf, unsigned short* y6, long long rows, int C, hipStream_t s) {
+  if (C % 8 || rows < 0) return hipErrorInvalidValue;
+  const long long total4 = rows * C / 4;
+  if (total4 == 0) return hipSuccess;
+  const long long nb = (total4 + 255) / 256;
+  const unsigned g = (unsigned)(nb < 8192 ? nb : 8192);
+  hipLaunchKernelGGL(silu_act_kernel, dim3(g), dim3(256), 0, s, x, yf, y6, rows, C);
   return hipGetLastError();
 }
 
@@ -247,13 +274,14 @@ __global__ void __launch_bounds__(256) split_planes_kernel(const float* __restri
        i4 += (long long)gridDim.x * blockDim.x) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(x + i4 * 4);
     const long long i = i4 * 4;
-    if (compact) store_bf16x4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
+    if (compact == 1) store_bf16x4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
+    else if (compact == 2) store_hm4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
     else store_planes4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
   }
 }
 
 hipError_t launch_split_planes(const float* x, unsigned short* y6, long long rows, int C, int compact, hipStream_t s) {
-  if (C % 8) return hipErrorInvalidValue;
+  if (C % 8 || compact < 0 || compact > 2 || (compact == 2 && C % 32)) return hipErrorInvalidValue;
   const long long total4 = rows * C / 4;
   unsigned g = (unsigned)((total4 + 255) / 256);
   if (g > 8192) g = 8192;
@@ -463,17 +491,22 @@ hipError_t launch_vq_rescore(const float* part_val, const int* part_idx, const f
   return hipGetLastError();
 }
 
-// out[r] = table[idx[r]] (batched_embedding / einx.get_at).  Negative indices wrap like torch
-// indexing; anything still outside [0, ntable) reads row 0 and is counted.
+// out[r] = table[idx[r]] (batched_embedding / einx.get_at).  With masked_row >= 0, index -1 reads
+// that row (the decode table's project_out(0) row: the reference masks code -1, residual_vq.py:120-127).
+// Other negative indices wrap like torch indexing; anything still outside [0, ntable) reads row 0
+// and is counted.
 __global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restrict__ table, int ntable,
                                                            const int32_t* __restrict__ idx, long long rows, int width,
-                                                           float* __restrict__ out, int32_t* n_invalid) {
+                                                           float* __restrict__ out, int32_t* n_invalid, int masked_row) {
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   int i = idx[row];
-  if (i < 0) i += ntable;
-  if (i < 0 || i >= ntable) {
+  if (i == -1 && masked_row >= 0)
+    i = masked_row;
+  else if (i < 0)
+    i += ntable;
+  if ((i < 0 || i >= ntable) && !(masked_row >= 0 && i == masked_row)) {
     if (lane == 0 && n_invalid) atomicAdd(n_invalid, 1);
     i = 0;
   }
@@ -484,10 +517,10 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restric
 }
 
 hipError_t launch_gather_rows(const float* table, int ntable, const int32_t* idx, long long rows, int width, float* out,
-                              int32_t* n_invalid, hipStream_t s) {
+                              int32_t* n_invalid, int masked_row, hipStream_t s) {
   if (width % 4) return hipErrorInvalidValue;
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, table, ntable, idx, rows,
-                     width, out, n_invalid);
+                     width, out, n_invalid, masked_row);
   return hipGetLastError();
 }
 

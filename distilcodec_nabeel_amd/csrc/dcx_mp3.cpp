@@ -13,8 +13,10 @@
 // Tables: the Huffman code books of Annex B (checked prefix-free and complete: Kraft sum 1) and the
 // synthesis window D[i] of Table 3-B.3 (integer multiples of 2^-16; its prototype lowpass is -3.01 dB
 // at pi/64 with > 104 dB stop-band attenuation, tests/test_mp3.py).
-// Not supported (the call fails with DCX_ERR_INVALID_ARG): MPEG-2 / 2.5 (LSF) streams, free-format
-// bitrates and intensity stereo (which LAME does not emit).
+// Not supported (the call fails with DCX_ERR_UNSUPPORTED, so callers can tell them from unreadable
+// data): MPEG-2 / 2.5 (LSF) streams, Layers I / II, free-format bitrates and intensity stereo (which
+// LAME does not emit).  Junk between frames is skipped like mpg123 / ffmpeg do: the scan resyncs on
+// the next header that the header after it confirms, and dcx_mp3_stats reports the skipped bytes.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -172,6 +174,16 @@ bool parse_header(const uint8_t* p, Header& h) {
   return true;
 }
 
+// A frame sync at p that is MPEG audio this decoder does not handle (MPEG-2 / 2.5, Layer I / II,
+// free format), with every header field in its valid range.
+bool unsupported_header(const uint8_t* p) {
+  const uint32_t v = (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+  if ((v >> 21) != 0x7FF) return false;
+  const int ver = (v >> 19) & 3, layer = (v >> 17) & 3, bi = (v >> 12) & 15, ri = (v >> 10) & 3;
+  if (ver == 1 || layer == 0 || bi == 15 || ri == 3) return false;  // reserved values: not a header
+  return ver != 3 || layer != 1 || bi == 0;
+}
+
 struct Bits {
   const uint8_t* p;
   size_t n, pos;  // bits
@@ -269,6 +281,8 @@ class Decoder {
     }
   }
 
+  bool unsupported = false;  // the last failure was a format feature, not bad data
+
   // Decodes one frame (header already parsed) to 1152 samples per channel (out[ch][1152]).
   // Returns false when the frame is not decodable (reservoir underflow, bad data, unsupported).
   bool frame(const uint8_t* f, const Header& h, float* out[2], std::string& err) {
@@ -282,7 +296,8 @@ class Decoder {
     SideInfo si;
     parse_side(sb, h.channels, si);
     if (h.mode == 1 && (h.mode_ext & 1)) {
-      err = "intensity stereo is not supported";
+      err = "unsupported MP3 feature: intensity stereo";
+      unsupported = true;
       return false;
     }
     const size_t have = res_.size();
@@ -556,17 +571,32 @@ struct Stream {
   int channels = 0, rate = 0;
   long long frames = 0;     // audio frames
   long long skip = 0, total = -1;  // gapless: leading samples to drop, samples to keep (-1: all)
+  std::vector<size_t> offsets;     // of every audio frame
+  long long junk = 0;       // bytes skipped between frames to resync
 };
 
-bool scan(const uint8_t* d, size_t n, Stream& s, std::string& err) {
+// A frame header at p whose successor (at p + its length) is a header too, or which ends the data.
+bool confirmed_header(const uint8_t* d, size_t n, size_t p) {
+  Header g, g2;
+  if (p + 4 > n || !parse_header(d + p, g) || p + g.bytes > n) return false;
+  return p + g.bytes == n || p + g.bytes + 4 > n || parse_header(d + p + g.bytes, g2);
+}
+
+// 0 = ok, DCX_ERR_INVALID_ARG = no decodable stream, DCX_ERR_UNSUPPORTED = MPEG audio of a kind
+// this decoder does not handle.
+int scan(const uint8_t* d, size_t n, Stream& s, std::string& err) {
   size_t i = 0;
   if (n >= 10 && d[0] == 'I' && d[1] == 'D' && d[2] == '3')
     i = 10 + ((size_t)(d[6] & 127) << 21 | (size_t)(d[7] & 127) << 14 | (size_t)(d[8] & 127) << 7 | (d[9] & 127));
+  if (i + 4 <= n && unsupported_header(d + i)) {
+    err = "unsupported MP3 stream: MPEG-2/2.5, Layer I/II or free-format (only MPEG-1 Layer III is decoded)";
+    return DCX_ERR_UNSUPPORTED;
+  }
   Header h;
   while (i + 4 <= n && !parse_header(d + i, h)) ++i;
   if (i + 4 > n) {
     err = "no MPEG-1 Layer III frame found";
-    return false;
+    return DCX_ERR_INVALID_ARG;
   }
   s.first = i;
   s.channels = h.channels;
@@ -589,7 +619,16 @@ bool scan(const uint8_t* d, size_t n, Stream& s, std::string& err) {
   }
   for (size_t p = s.first; p + 4 <= n;) {
     Header g;
-    if (!parse_header(d + p, g) || p + g.bytes > n) break;
+    if (!parse_header(d + p, g) || p + g.bytes > n) {
+      // junk or a damaged frame: resync on the next header confirmed by the one after it
+      size_t q = p + 1;
+      while (q + 4 <= n && !confirmed_header(d, n, q)) ++q;
+      if (q + 4 > n) break;  // trailing junk (e.g. an ID3v1 tag) or a truncated last frame
+      s.junk += (long long)(q - p);
+      p = q;
+      continue;
+    }
+    s.offsets.push_back(p);
     ++s.frames;
     p += g.bytes;
   }
@@ -598,11 +637,11 @@ bool scan(const uint8_t* d, size_t n, Stream& s, std::string& err) {
     s.total = s.frames * 1152;
   }
   s.total = std::max(0LL, std::min(s.total, s.frames * 1152 - s.skip));
-  return true;
+  return DCX_OK;
 }
 
 thread_local std::string g_mp3_err;
-thread_local long long g_mp3_stats[2];
+thread_local long long g_mp3_stats[4];  // granules, exact granules, junk bytes, bad frames
 
 }  // namespace
 
@@ -610,7 +649,8 @@ extern "C" int dcx_mp3_info(const uint8_t* data, size_t nbytes, int64_t* samples
                             int32_t* channels) {
   if (!data || !samples || !sample_rate || !channels) return DCX_ERR_INVALID_ARG;
   Stream s;
-  if (!scan(data, nbytes, s, g_mp3_err)) return DCX_ERR_INVALID_ARG;
+  const int rc = scan(data, nbytes, s, g_mp3_err);
+  if (rc != DCX_OK) return rc;
   *samples = s.total;
   *sample_rate = s.rate;
   *channels = s.channels;
@@ -619,9 +659,10 @@ extern "C" int dcx_mp3_info(const uint8_t* data, size_t nbytes, int64_t* samples
 
 extern "C" int dcx_mp3_decode(const uint8_t* data, size_t nbytes, float* out, int64_t capacity) {
   if (!data || !out) return DCX_ERR_INVALID_ARG;
-  g_mp3_stats[0] = g_mp3_stats[1] = 0;
+  g_mp3_stats[0] = g_mp3_stats[1] = g_mp3_stats[2] = g_mp3_stats[3] = 0;
   Stream s;
-  if (!scan(data, nbytes, s, g_mp3_err)) return DCX_ERR_INVALID_ARG;
+  const int rc = scan(data, nbytes, s, g_mp3_err);
+  if (rc != DCX_OK) return rc;
   if (capacity < s.total) {
     g_mp3_err = "output capacity below dcx_mp3_info's sample count";
     return DCX_ERR_INVALID_ARG;
@@ -630,8 +671,8 @@ extern "C" int dcx_mp3_decode(const uint8_t* data, size_t nbytes, float* out, in
   std::vector<float> pcm[2];
   for (int ch = 0; ch < s.channels; ++ch) pcm[ch].assign(1152, 0.f);
   long long produced = 0;  // decoded samples per channel so far
-  size_t p = s.first;
   for (long long f = 0; f < s.frames; ++f) {
+    const size_t p = s.offsets[(size_t)f];
     Header h;
     if (!parse_header(data + p, h)) break;
     float* o[2] = {pcm[0].data(), s.channels > 1 ? pcm[1].data() : nullptr};
@@ -639,16 +680,22 @@ extern "C" int dcx_mp3_decode(const uint8_t* data, size_t nbytes, float* out, in
       g_mp3_err = "channel count or sample rate changes inside the stream";
       return DCX_ERR_INVALID_ARG;
     }
-    if (!dec.frame(data + p, h, o, g_mp3_err)) return DCX_ERR_INVALID_ARG;
+    if (!dec.frame(data + p, h, o, g_mp3_err)) {
+      if (dec.unsupported) return DCX_ERR_UNSUPPORTED;
+      // a damaged frame (bad Huffman data, a reservoir broken by junk): silence for it and carry on,
+      // as mpg123 / ffmpeg conceal decode errors; counted in dcx_mp3_bad_frames
+      for (int ch = 0; ch < s.channels; ++ch) std::memset(o[ch], 0, sizeof(float) * 1152);
+      ++g_mp3_stats[3];
+    }
     for (int i = 0; i < 1152; ++i, ++produced) {
       const long long k = produced - s.skip;
       if (k < 0 || k >= s.total) continue;
       for (int ch = 0; ch < s.channels; ++ch) out[(long long)ch * s.total + k] = pcm[ch][i];
     }
-    p += h.bytes;
   }
   g_mp3_stats[0] = dec.stats_[0];
   g_mp3_stats[1] = dec.stats_[1];
+  g_mp3_stats[2] = s.junk;
   return DCX_OK;
 }
 
@@ -658,5 +705,9 @@ extern "C" int dcx_mp3_stats(int64_t* granules, int64_t* exact) {
   *exact = g_mp3_stats[1];
   return DCX_OK;
 }
+
+extern "C" int64_t dcx_mp3_junk_bytes(void) { return g_mp3_stats[2]; }
+
+extern "C" int64_t dcx_mp3_bad_frames(void) { return g_mp3_stats[3]; }
 
 extern "C" const char* dcx_mp3_last_error(void) { return g_mp3_err.c_str(); }

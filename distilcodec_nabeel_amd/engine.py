@@ -133,14 +133,20 @@ class NativeCodec:
     # ------------------------------------------------------------------ stages
     # Every stage takes an optional caller-owned workspace `ws` (see `workspace`): a captured hipGraph
     # must keep the buffer it was recorded with.
-    def mel(self, audio: torch.Tensor, ws: torch.Tensor | None = None) -> torch.Tensor:
-        """audio (B, N) fp32 (with the reference's leading zero) -> mel (B, T, n_mels)."""
+    def mel(self, audio: torch.Tensor, ws: torch.Tensor | None = None, linear: bool = False):
+        """audio (B, N) fp32 (with the reference's leading zero) -> mel (B, T, n_mels); with
+        `linear`, also log(clamp(|STFT|, 1e-5)) (B, T, n_fft/2 + 1) (return_linear, mel_spec.py:119-120)."""
         audio = self._dev(audio, torch.float32)
         B, N = audio.shape
         T = self.num_frames(N)
         out = torch.empty(B, T, self.n_mels, device=self.device)
         ws = self.workspace(B, T, ws)
         with torch.cuda.device(self.device):
+            if linear:
+                lin = torch.empty(B, T, self.cfg["spec_transform"]["n_fft"] // 2 + 1, device=self.device)
+                self._check(self.L.dcx_mel_linear(self.h, self._ptr(audio), B, N, self._ptr(out), self._ptr(lin),
+                                                  self._ptr(ws), ws.numel(), self._stream()))
+                return out, lin
             self._check(self.L.dcx_mel(self.h, self._ptr(audio), B, N, self._ptr(out), self._ptr(ws), ws.numel(), self._stream()))
         return out
 
@@ -202,6 +208,29 @@ class NativeCodec:
             self._check(self.L.dcx_encode_decode(self.h, self._ptr(audio), B, N, self._ptr(codes), self._ptr(wav), self._ptr(ws),
                                                  ws.numel(), self._stream()))
         return codes, wav
+
+    def module(self, name: str, x: torch.Tensor) -> torch.Tensor:
+        """One reference module by its state-dict prefix (dcx_module_forward): x channels-last
+        (B, L, C) fp32 -> y (see the header for shapes; int32 codes for "quantizer.search")."""
+        x = self._dev(x, torch.float32)
+        B, L, C = x.shape
+        n = name.encode()
+        need = int(self.L.dcx_module_workspace_size(self.h, n, B, L))
+        if need == 0:
+            raise ValueError(f"unknown module {name!r}")
+        if name == "quantizer.search":
+            y = torch.empty(B, L, dtype=torch.int32, device=self.device)
+        elif name.startswith("generator.ups."):
+            i = int(name.split(".")[2])
+            d = self.cfg["decoder"]
+            y = torch.empty(B, L * d["upsample_rates"][i], d["upsample_initial_channel"] // 2 ** (i + 1), device=self.device)
+        else:
+            y = torch.empty(B, L, C, device=self.device)
+        ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            self._check(self.L.dcx_module_forward(self.h, n, self._ptr(x), B, L, self._ptr(y), self._ptr(ws), ws.numel(),
+                                                  self._stream()))
+        return y
 
     def transpose(self, x: torch.Tensor) -> torch.Tensor:
         """(B, R, C) -> (B, C, R) contiguous, on device, by the HIP transpose kernel."""

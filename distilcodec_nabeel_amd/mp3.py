@@ -17,7 +17,18 @@ from . import _native
 
 
 class Mp3Error(ValueError):
-    pass
+    """The data is not a decodable MPEG audio stream (what librosa would also fail to read)."""
+
+
+class Mp3Unsupported(Mp3Error):
+    """A valid MPEG audio stream using a feature this decoder lacks (MPEG-2/2.5, Layer I/II, free
+    format, intensity stereo).  librosa would decode it, so callers must not treat it as an
+    unreadable file: `DistilCodec.encode` re-raises it instead of substituting noise."""
+
+
+def _raise(L, rc):
+    msg = L.dcx_mp3_last_error().decode()
+    raise (Mp3Unsupported if rc == _native.DCX_ERR_UNSUPPORTED else Mp3Error)(msg)
 
 
 def decode_mp3_bytes(data: bytes) -> tuple[np.ndarray, int]:
@@ -25,11 +36,13 @@ def decode_mp3_bytes(data: bytes) -> tuple[np.ndarray, int]:
     L = _native.lib()
     buf = ctypes.create_string_buffer(data, len(data))
     n, sr, ch = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32()
-    if L.dcx_mp3_info(buf, len(data), ctypes.byref(n), ctypes.byref(sr), ctypes.byref(ch)) != 0:
-        raise Mp3Error(L.dcx_mp3_last_error().decode())
+    rc = L.dcx_mp3_info(buf, len(data), ctypes.byref(n), ctypes.byref(sr), ctypes.byref(ch))
+    if rc != 0:
+        _raise(L, rc)
     out = np.zeros((ch.value, max(n.value, 1)), np.float32)
-    if L.dcx_mp3_decode(buf, len(data), out.ctypes.data, n.value) != 0:
-        raise Mp3Error(L.dcx_mp3_last_error().decode())
+    rc = L.dcx_mp3_decode(buf, len(data), out.ctypes.data, n.value)
+    if rc != 0:
+        _raise(L, rc)
     return np.ascontiguousarray(out[:, : n.value].T), sr.value
 
 
@@ -44,3 +57,13 @@ def last_stats() -> tuple[int, int]:
     g, e = ctypes.c_int64(), ctypes.c_int64()
     _native.lib().dcx_mp3_stats(ctypes.byref(g), ctypes.byref(e))
     return g.value, e.value
+
+
+def last_junk_bytes() -> int:
+    """Bytes the last decode on this thread skipped to resync on a frame header (0: clean stream)."""
+    return int(_native.lib().dcx_mp3_junk_bytes())
+
+
+def last_bad_frames() -> int:
+    """Frames of the last decode on this thread whose data was damaged; they decode as silence."""
+    return int(_native.lib().dcx_mp3_bad_frames())

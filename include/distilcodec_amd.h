@@ -35,7 +35,8 @@ enum {
   DCX_ERR_STATE = -3,          /* call order violated (e.g. stage call before dcx_finalize) */
   DCX_ERR_HIP = -4,            /* a HIP runtime call failed */
   DCX_ERR_OOM = -5,            /* device allocation failed (dcx_finalize only) */
-  DCX_ERR_WORKSPACE = -6       /* workspace smaller than dcx_workspace_size() */
+  DCX_ERR_WORKSPACE = -6,      /* workspace smaller than dcx_workspace_size() */
+  DCX_ERR_UNSUPPORTED = -7     /* input in a format this build does not decode (dcx_mp3_*) */
 };
 
 typedef struct dcx_codec dcx_codec;
@@ -97,6 +98,10 @@ size_t dcx_workspace_size(const dcx_codec* h, int32_t batch, int64_t frames);
  * reference's 1-sample left pad); mel: [B][T][n_mels]. */
 int dcx_mel(dcx_codec* h, const float* audio, int32_t batch, int64_t n_samples, float* mel,
             void* workspace, size_t ws_bytes, void* stream);
+/* dcx_mel plus the linear spectrogram of LogMelSpectrogram.forward(return_linear=True)
+ * (mel_spec.py:119-120): log_linear [B][T][n_fft/2 + 1] = log(clamp(|STFT|, 1e-5)). */
+int dcx_mel_linear(dcx_codec* h, const float* audio, int32_t batch, int64_t n_samples, float* mel, float* log_linear,
+                   void* workspace, size_t ws_bytes, void* stream);
 
 /* ConvNeXt encoder.  Replaces ConvNeXtEncoder.forward (encoders.py:68-76).
  * mel: [B][T][n_mels] -> feat: [B][T][enc_dims[3]]. */
@@ -113,8 +118,10 @@ int dcx_vq_encode(dcx_codec* h, const float* feat, int32_t batch, int64_t frames
                   void* workspace, size_t ws_bytes, void* stream);
 
 /* DownsampleGRVQ.decode (grfvq.py:141-146): codes [B][T] int32 -> z [B][T][vq_dim].
- * Negative codes in [-codebook_size, 0) wrap to code + codebook_size, like the torch indexing of
- * the reference's gather (distil_codec.py:584-586, residual_vq.py:123).  Codes still outside
+ * Code -1 is the reference's masked code (residual_vq.py:120-127: fetched as code 0, then zeroed
+ * before project_out), so its frame decodes project_out(0) = the project_out bias.  Other negative
+ * codes in [-codebook_size, -1) wrap to code + codebook_size, like the torch indexing of the
+ * reference's gather (distil_codec.py:584-586, residual_vq.py:123).  Codes still outside
  * [0, codebook_size) read row 0 and are counted into *n_invalid (device int, may be NULL); the
  * Python surface raises IndexError for them before calling, as torch indexing would. */
 int dcx_vq_decode(dcx_codec* h, const int32_t* codes, int32_t batch, int64_t frames, float* z,
@@ -142,14 +149,20 @@ int dcx_resample_poly(const float* x, int32_t batch, int64_t n_in, int64_t x_str
  * path (meldataset.py:18-20, distil_codec.py:667; C1's test.mp3, README.md:116), with Xing/LAME
  * gapless trimming (encoder delay + 529 decoder-delay samples skipped, encoder padding dropped).
  * dcx_mp3_info: samples per channel, sample rate, channels.  dcx_mp3_decode: channel-major float
- * samples out[ch][samples] (capacity = samples per channel available).  MPEG-2/2.5, free format and
- * intensity stereo return DCX_ERR_INVALID_ARG; dcx_mp3_last_error() has the text (per thread).
+ * samples out[ch][samples] (capacity = samples per channel available).  MPEG-2/2.5, Layer I/II,
+ * free format and intensity stereo return DCX_ERR_UNSUPPORTED; data with no decodable frame returns
+ * DCX_ERR_INVALID_ARG; dcx_mp3_last_error() has the text (per thread).  Junk between frames is
+ * skipped by resyncing on the next header confirmed by its successor, as mpg123 / ffmpeg do.
  * dcx_mp3_stats: granules of the last decode, and how many of them ended their Huffman data exactly
- * at part2_3_length (a check on the code books). */
+ * at part2_3_length (a check on the code books).  dcx_mp3_junk_bytes: bytes the last decode skipped
+ * to resync (0 for a clean stream).  dcx_mp3_bad_frames: frames of the last decode whose data was
+ * damaged (e.g. cut by junk); they decode as silence, as mpg123 / ffmpeg conceal decode errors. */
 int dcx_mp3_info(const uint8_t* data, size_t nbytes, int64_t* samples, int32_t* sample_rate, int32_t* channels);
 int dcx_mp3_decode(const uint8_t* data, size_t nbytes, float* out, int64_t capacity);
 const char* dcx_mp3_last_error(void);
 int dcx_mp3_stats(int64_t* granules, int64_t* exact);
+int64_t dcx_mp3_junk_bytes(void);
+int64_t dcx_mp3_bad_frames(void);
 
 /* Batched 2-D transpose [B][R][C] -> [B][C][R] (channels-first <-> channels-last bridge). */
 int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int64_t cols, void* stream);
@@ -192,6 +205,27 @@ int dcx_conv_create(const float* weight, const float* bias, int32_t cin, int32_t
 int dcx_conv_forward(dcx_conv* c, int32_t gemm_mode, const float* x, int32_t batch, int64_t lin, float* y,
                      float* y_silu, const float* res, int32_t epi, void* stream);
 void dcx_conv_destroy(dcx_conv* c);
+
+/* Single reference modules, for per-module parity tests (tests/test_gpu_modules.py against the
+ * reference's own module outputs, tests/golden/modules.npz).  `module` is the module's state-dict
+ * prefix in the reference; the call runs it on the handle's packed weights through the same kernels
+ * and launch code the stages use, in the handle's arithmetic mode.  x / y are channels-last fp32
+ * [B][rows][C] unless noted:
+ *   "encoder.stages.<i>.<j>", "quantizer.downsample.0.1", "quantizer.upsample.0.1": ConvNeXtBlock
+ *       (convnext_utils.py:263-282);
+ *   "encoder.downsample_layers.0.1", "encoder.downsample_layers.<i>.0", "encoder.norm": channels-first
+ *       LayerNorm (convnext_utils.py:186-213);
+ *   "generator.ups.<i>": ConvTranspose1d, y [B][rows * rate][Cout] (generators.py:29-116);
+ *   "generator.resblocks.<i>.blocks.<j>": ResBlock1 (convnext_utils.py:106-113), per-conv launches;
+ *   "generator.resblocks.<i>": the stage's ParralelBlock (convnext_utils.py:137-138) as the generator
+ *       runs it, with the SiLU that follows it fused: y = silu(mean of the ResBlock1s) (fused pair
+ *       kernels at C = 32 / 64);
+ *   "quantizer.search": nearest code (vector_quantize_pytorch.py:41-45, 496-506) of x_pjt_in rows
+ *       x [B][rows][codebook_dim]; y = int32 codes [B][rows] (x6 and fp32 modes).
+ * Unknown names return DCX_ERR_INVALID_ARG.  dcx_module_workspace_size returns 0 for them. */
+size_t dcx_module_workspace_size(const dcx_codec* h, const char* module, int32_t batch, int64_t rows);
+int dcx_module_forward(dcx_codec* h, const char* module, const float* x, int32_t batch, int64_t rows, void* y,
+                       void* workspace, size_t ws_bytes, void* stream);
 
 /* VQ search diagnostics (x6 mode): the search is a bf16x3 prefilter whose winner is certified
  * by a rigorous error bound; rows with more than one code inside the bound are rescored in fp64.

@@ -58,8 +58,10 @@ def melscale_fbanks_slaney(n_freqs=513, f_min=0.0, f_max=12000.0, n_mels=128, sa
     return fb.astype(np.float32)
 
 
-def log_mel(audio: torch.Tensor, fb: torch.Tensor | None = None, n_fft=1024, hop=256, win=1024) -> torch.Tensor:
-    """LogMelSpectrogram.forward (mel_spec.py:109-122) on (B, N) or (B, 1, N) audio -> (B, 128, T)."""
+def log_mel(audio: torch.Tensor, fb: torch.Tensor | None = None, n_fft=1024, hop=256, win=1024,
+            return_linear: bool = False):
+    """LogMelSpectrogram.forward (mel_spec.py:109-122) on (B, N) or (B, 1, N) audio -> (B, 128, T);
+    with return_linear also compress(linear) (B, n_fft/2 + 1, T) (:119-120)."""
     if audio.ndim == 3:
         audio = audio.squeeze(1)
     # LinearSpectrogram.forward, mel_spec.py:26-57
@@ -73,7 +75,10 @@ def log_mel(audio: torch.Tensor, fb: torch.Tensor | None = None, n_fft=1024, hop
         fb = torch.from_numpy(melscale_fbanks_slaney()).to(audio.dtype)
     # apply_mel_scale (mel_spec.py:106-107) then compress (mel_spec.py:100-101)
     x = torch.matmul(spec.transpose(-1, -2), fb).transpose(-1, -2)
-    return torch.log(torch.clamp(x, min=1e-5))
+    x = torch.log(torch.clamp(x, min=1e-5))
+    if return_linear:
+        return x, torch.log(torch.clamp(spec, min=1e-5))
+    return x
 
 
 def pad_batch(clips: list[np.ndarray]) -> tuple[torch.Tensor, list[int]]:
@@ -194,9 +199,12 @@ def _vq_upsample(x, sd_q, dtype):
 
 def vq_decode(codes_bt: torch.Tensor, sd_q, dtype=torch.float32):
     """DownsampleGRVQ.decode (grfvq.py:141-146) with indices laid out (G=1, B, T, R=1):
-    gather (residual_vq.py:123) -> sum over q -> project_out (:138) -> upsample."""
+    gather (residual_vq.py:123) -> sum over q -> project_out (:138) -> upsample.  Code -1 is the
+    masked code (residual_vq.py:120-127): fetched as code 0, then zeroed before project_out; other
+    negative codes wrap like torch indexing."""
     embed = codebook(sd_q, dtype)
-    q = embed[codes_bt]
+    mask = codes_bt == -1
+    q = embed[codes_bt.masked_fill(mask, 0)].masked_fill(mask[..., None], 0.0)
     q_down = F.linear(q, _t(sd_q, "grvq.rvqs.0.project_out.weight", dtype), _t(sd_q, "grvq.rvqs.0.project_out.bias", dtype))
     return _vq_upsample(q_down.mT, sd_q, dtype)
 
@@ -216,6 +224,15 @@ def _resblock1(x, sd, p, k, dils, dtype):
     return x
 
 
+def parallel_block(x, sd, i, cfg_decoder, dtype=torch.float32):
+    """ParralelBlock.forward (convnext_utils.py:137-138) of generator stage i: the mean of its
+    ResBlock1s (convnext_utils.py:106-113), stacked in block order."""
+    d = cfg_decoder
+    outs = [_resblock1(x, sd, f"resblocks.{i}.blocks.{b}", rk, dl, dtype)
+            for b, (rk, dl) in enumerate(zip(d["resblock_kernel_sizes"], d["resblock_dilation_sizes"]))]
+    return torch.stack(outs, dim=0).mean(dim=0)
+
+
 def generator(z, sd, cfg_decoder, dtype=torch.float32, stages=None):
     d = cfg_decoder
     x = F.conv1d(z.to(dtype), _w(sd, "conv_pre", dtype), _t(sd, "conv_pre.bias", dtype), padding=(d["pre_conv_kernel_size"] - 1) // 2)
@@ -224,9 +241,7 @@ def generator(z, sd, cfg_decoder, dtype=torch.float32, stages=None):
         u, k = d["upsample_rates"][i], d["upsample_kernel_sizes"][i]
         x = F.silu(x)
         x = F.conv_transpose1d(x, _w(sd, f"ups.{i}", dtype), _t(sd, f"ups.{i}.bias", dtype), stride=u, padding=(k - u) // 2)
-        outs = [_resblock1(x, sd, f"resblocks.{i}.blocks.{b}", rk, dl, dtype)
-                for b, (rk, dl) in enumerate(zip(d["resblock_kernel_sizes"], d["resblock_dilation_sizes"]))]
-        x = torch.stack(outs, dim=0).mean(dim=0)
+        x = parallel_block(x, sd, i, d, dtype)
     if stages is not None:
         return x
     x = F.silu(x)

@@ -36,6 +36,12 @@ def resample(x: np.ndarray, sr_in: int, sr_out: int) -> np.ndarray:
     if up == down:
         return x.copy()
     h, pre = design(up, down)
+    return apply_poly(x, h, pre, up, down)
+
+
+def apply_poly(x: np.ndarray, h: np.ndarray, pre: int, up: int, down: int) -> np.ndarray:
+    """The polyphase form of dcx_resample_poly in fp64 for any prototype filter h."""
+    x = np.asarray(x, dtype=np.float64)
     n = x.shape[-1]
     no = -(-n * up // down)
     t = (np.arange(no) + pre) * down
@@ -47,3 +53,43 @@ def resample(x: np.ndarray, sr_in: int, sr_out: int) -> np.ndarray:
         if ok.any():
             out[..., ok] += h[k] * x[..., m[ok]]
     return out
+
+
+def torchaudio_resample(waveform, orig_freq: int, new_freq: int, lowpass_filter_width: int = 6,
+                        rolloff: float = 0.99):
+    """`torchaudio.functional.resample` with its defaults (resampling_method="sinc_interp_hann"),
+    the resampler of LogMelSpectrogram.forward(sample_rate=...) (mel_spec.py:112-113; torchaudio
+    2.4.1 pinned at requirements.txt:17).  Restated from torchaudio's published
+    `_get_sinc_resample_kernel` / `_apply_sinc_resample_kernel`: the kernel is built in the input's
+    dtype, the signal zero-padded by (width, width + orig) and convolved with stride orig, one output
+    channel per phase.  torchaudio is not installed here, so parity is UNPINNED (no reference-held
+    output exists); tests pin the GPU path to this restatement."""
+    import math
+
+    import torch
+
+    x = torch.as_tensor(waveform)
+    if orig_freq == new_freq:
+        return x
+    g = math.gcd(int(orig_freq), int(new_freq))
+    orig, new = int(orig_freq) // g, int(new_freq) // g
+    dtype = x.dtype
+    base_freq = min(orig, new) * rolloff
+    width = math.ceil(lowpass_filter_width * orig / base_freq)
+    idx = torch.arange(-width, width + orig, dtype=dtype)[None, None] / orig
+    t = torch.arange(0, -new, -1, dtype=dtype)[:, None, None] / new + idx
+    t *= base_freq
+    t = t.clamp_(-lowpass_filter_width, lowpass_filter_width)
+    window = torch.cos(t * math.pi / lowpass_filter_width / 2) ** 2
+    t *= math.pi
+    scale = base_freq / orig
+    kernels = torch.where(t == 0, torch.tensor(1.0).to(t), t.sin() / t)
+    kernels *= window * scale
+    shape = x.shape
+    w = x.reshape(-1, shape[-1])
+    n = w.shape[-1]
+    w = torch.nn.functional.pad(w, (width, width + orig))
+    y = torch.nn.functional.conv1d(w[:, None], kernels, stride=orig)
+    y = y.transpose(1, 2).reshape(w.shape[0], -1)
+    target = int(math.ceil(new * n / orig))
+    return y[..., :target].reshape(shape[:-1] + (-1,))

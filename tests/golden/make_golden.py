@@ -21,7 +21,8 @@ Fixtures
 * `modules.npz`     : per-module cases called on the reference's own modules: ConvNeXtBlock(256),
                       channels-first LayerNorm(256), ResBlock1(64, k=11), ParralelBlock(32),
                       each ConvTranspose1d of the generator, EuclideanCodebook search on a
-                      1024-code slice.
+                      1024-code slice, `quantizer.decode` of codes holding the masked code -1,
+                      and `spec_transform(..., return_linear=True)` of e2e_batch clip 0.
 """
 from __future__ import annotations
 
@@ -157,6 +158,15 @@ def main():
         cb.codebook_size = embed.shape[0]
         mods["vq1024_in"], mods["vq1024_codes"], mods["vq1024_quant"] = _np(x), _np(ind[0]).astype(np.int64), _np(q[0])
         mods["mel_fb"] = _np(codec.spec_transform.fb)
+        # masked code -1 (residual_vq.py:120-127) and a wrapping -32768 through quantizer.decode
+        mc = np.random.Generator(np.random.PCG64(7)).integers(0, 32768, 24)
+        mc[[0, 5, 6, 23]] = -1
+        mc[2] = -32768
+        zq = codec.quantizer.decode(torch.from_numpy(mc)[None, None, :, None])
+        mods["masked_codes"], mods["masked_z"] = mc.astype(np.int64), _np(zq)
+        # LogMelSpectrogram.forward(return_linear=True) (mel_spec.py:119-120) on e2e_batch clip 0
+        mel_l, lin_l = codec.spec_transform(torch.from_numpy(out["audio"][:1])[:, None, :], return_linear=True)
+        mods["linear_mel"], mods["linear_log"] = _np(mel_l), _np(lin_l)
     np.savez_compressed(os.path.join(HERE, "modules.npz"), **mods)
     print("modules", sorted(mods))
     for f in ("e2e_batch.npz", "e2e_3s.npz", "e2e_real.npz", "modules.npz"):

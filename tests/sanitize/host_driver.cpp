@@ -75,6 +75,14 @@ static int run_mp3(const char* path) {
     }
     decode_any(c);
   }
+  // junk runs inserted anywhere (the scan resyncs on confirmed headers; damaged frames are silenced)
+  for (int it = 0; it < 100; ++it) {
+    std::vector<uint8_t> c = d;
+    std::vector<uint8_t> junk(1 + rnd() % 2000);
+    for (auto& b : junk) b = (uint8_t)rnd();
+    c.insert(c.begin() + rnd() % c.size(), junk.begin(), junk.end());
+    decode_any(c);
+  }
   // garbage and frame-sync lookalikes
   for (int it = 0; it < 200; ++it) {
     std::vector<uint8_t> g(1 + rnd() % 4096);
@@ -85,7 +93,7 @@ static int run_mp3(const char* path) {
   CHECK(dcx_mp3_info(nullptr, 10, nullptr, nullptr, nullptr) != DCX_OK);
   float tiny[4];
   CHECK(dcx_mp3_decode(d.data(), d.size(), tiny, 4) != DCX_OK);  // capacity below the sample count
-  std::printf("mp3: %zu bytes, 110 prefixes, 400 corrupted and 200 garbage inputs decoded or rejected\n", d.size());
+  std::printf("mp3: %zu bytes, 110 prefixes, 400 corrupted, 100 junk-inserted and 200 garbage inputs decoded or rejected\n", d.size());
   return g_fail;
 }
 

@@ -87,6 +87,28 @@ def test_decode_from_codes(codec, golden):
     assert torch.equal(codec.decode_from_codes(toks_neg), wav2)
 
 
+def test_decode_masked_code(codec, state):
+    """Code -1 is the reference's masked code (residual_vq.py:120-127): it is fetched as code 0 and
+    zeroed before project_out, so its frame decodes the project_out bias.  -32768 still wraps to 0,
+    and a token one below the offset (minus_token_offset) becomes code -1."""
+    from oracle import reference_cpu as R
+
+    rng = np.random.RandomState(5)
+    codes = rng.randint(0, 32768, size=60)
+    codes[[0, 7, 8, 30, 59]] = -1
+    codes[[3, 40]] = -32768
+    wav = codec.decode_from_codes(codes.tolist(), minus_token_offset=False)
+    z = R.vq_decode(torch.from_numpy(codes)[None], state["quantizer"])
+    ref = R.generator(z, state["generator"], codec.decoder_config)
+    assert _snr(wav[0, 0], ref[0, 0].numpy()) >= 80
+    # not the wrapped code 32767
+    wrapped = codes.copy()
+    wrapped[wrapped == -1] = 32767
+    assert not torch.equal(wav, codec.decode_from_codes(wrapped.tolist(), minus_token_offset=False))
+    toks = (codes + codec.tokens_id_offset).tolist()
+    assert torch.equal(codec.decode_from_codes(toks), wav)
+
+
 def test_decode_from_codes_batch(codec, golden):
     g = golden["e2e_batch"]
     lists = [g["codes"][0].tolist(), g["codes"][1, :66].tolist()]

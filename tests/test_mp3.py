@@ -120,3 +120,65 @@ def test_truncated_and_garbage_input():
     assert sr == 44100 and 0 < len(y) < 88 * 1152 - 576 - 1472
     with pytest.raises(mp3.Mp3Error):
         mp3.decode_mp3_bytes(bytes(range(256)) * 8)
+
+
+def _frame_offsets(data: bytes) -> list:
+    """Offsets of the MPEG-1 Layer III frames after the ID3v2 tag (test helper)."""
+    rates, kbps = (44100, 48000, 32000), (0, 32, 40, 48, 56, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320)
+    i = 0
+    if data[:3] == b"ID3":
+        i = 10 + ((data[6] & 127) << 21 | (data[7] & 127) << 14 | (data[8] & 127) << 7 | (data[9] & 127))
+    out = []
+    while i + 4 <= len(data) and data[i] == 0xFF and (data[i + 1] & 0xFE) == 0xFA:
+        out.append(i)
+        i += 144000 * kbps[data[i + 2] >> 4] // rates[(data[i + 2] >> 2) & 3] + ((data[i + 2] >> 1) & 1)
+    return out
+
+
+def test_junk_between_frames_resyncs():
+    """Junk inside the stream: the decoder skips it like mpg123 / ffmpeg, resyncing on the
+    next header that the following header confirms; a clean frame boundary gives the same samples."""
+    from distilcodec_nabeel_amd import mp3
+
+    data = open(MP3, "rb").read()
+    clean, sr = mp3.decode_mp3_bytes(data)
+    assert mp3.last_junk_bytes() == 0
+    offs = _frame_offsets(data)
+    assert len(offs) >= 80
+    junk = np.random.RandomState(3).randint(0, 256, 517).astype(np.uint8).tobytes()
+    k = offs[40]
+    y, sr2 = mp3.decode_mp3_bytes(data[:k] + junk + data[k:])
+    assert mp3.last_junk_bytes() == 517 and mp3.last_bad_frames() == 0 and sr2 == sr
+    assert np.array_equal(y, clean)
+    # junk cutting frame 40 short: its header still declares a full frame, whose tail is junk; the scan
+    # resyncs on frame 41.  Damaged frames decode as silence (error concealment), the stream goes on
+    # with the same length, and the audio before the damage is unchanged.
+    y2, _ = mp3.decode_mp3_bytes(data[:k + 100] + junk + data[offs[41]:])
+    assert mp3.last_junk_bytes() > 0 and len(y2) == len(clean)
+    n_ok = 38 * 1152 - (576 + 1152 - 529)  # whole frames before the damage, after the gapless skip
+    assert np.array_equal(y2[:n_ok], clean[:n_ok])
+    assert np.isfinite(y2).all()
+
+
+@pytest.mark.parametrize("header,what", [
+    (b"\xff\xf3\x64\xc4", "MPEG-2 Layer III"),
+    (b"\xff\xe3\x64\xc4", "MPEG-2.5 Layer III"),
+    (b"\xff\xfd\x94\x44", "MPEG-1 Layer II"),
+    (b"\xff\xfb\x04\x44", "MPEG-1 Layer III free format"),
+])
+def test_unsupported_streams_raise_loudly(tmp_path, cfg, header, what):
+    """MPEG audio of a kind the host decoder lacks raises Mp3Unsupported, and the path-input encode
+    re-raises it instead of substituting noise (librosa would decode these files)."""
+    from distilcodec_nabeel_amd import DistilCodec, mp3
+
+    data = (header + bytes(400)) * 20
+    with pytest.raises(mp3.Mp3Unsupported):
+        mp3.decode_mp3_bytes(data)
+    p = tmp_path / "lsf.mp3"
+    p.write_bytes(b"ID3\x03\x00\x00\x00\x00\x00\x00" + data)
+    with pytest.raises(mp3.Mp3Unsupported):
+        DistilCodec(cfg)._read_audio_files([str(p)])
+    # a corrupt file is still an ordinary read failure (the reference's noise fallback applies)
+    with pytest.raises(mp3.Mp3Error) as e:
+        mp3.decode_mp3_bytes(b"\xff\xfb\xf0\x00" + bytes(300))
+    assert not isinstance(e.value, mp3.Mp3Unsupported)

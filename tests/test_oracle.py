@@ -55,10 +55,33 @@ def test_modules(golden, state, cfg):
             y = torch.nn.functional.conv_transpose1d(x, R._w(sd_g, f"ups.{i}", torch.float32),
                                                      torch.from_numpy(sd_g[f"ups.{i}.bias"]), stride=u, padding=(k - u) // 2)
             assert _rel(y, m[f"ups{i}_out"]) < 1e-5, i
+        x = torch.from_numpy(m["parallel32_in"])
+        assert _rel(R.parallel_block(x, sd_g, 4, d, torch.float32), m["parallel32_out"]) < 1e-5
         emb = R.codebook(state["quantizer"])[:1024]
         idx = R.vq_search(torch.from_numpy(m["vq1024_in"]), emb)
         assert np.array_equal(idx.numpy(), m["vq1024_codes"])
         assert np.array_equal(emb[idx].numpy(), m["vq1024_quant"])
+
+
+def test_masked_code_decode(golden, state):
+    """quantizer.decode with the masked code -1 (residual_vq.py:120-127) and a wrapping -32768."""
+    m = golden["modules"]
+    with torch.no_grad():
+        z = R.vq_decode(torch.from_numpy(m["masked_codes"])[None], state["quantizer"])
+    assert _rel(z, m["masked_z"]) < 1e-5
+    wrapped = m["masked_codes"].copy()
+    wrapped[wrapped == -1] = 32767  # plain torch wrapping would give another result
+    with torch.no_grad():
+        assert _rel(R.vq_decode(torch.from_numpy(wrapped)[None], state["quantizer"]), m["masked_z"]) > 1e-3
+
+
+def test_return_linear(golden):
+    """LogMelSpectrogram.forward(return_linear=True) (mel_spec.py:119-120)."""
+    m, g = golden["modules"], golden["e2e_batch"]
+    mel, lin = R.log_mel(torch.from_numpy(g["audio"][:1]), return_linear=True)
+    assert lin.shape == m["linear_log"].shape == (1, 513, 93)
+    assert np.abs(mel.numpy() - m["linear_mel"]).max() < 1e-4
+    assert np.abs(lin.numpy() - m["linear_log"]).max() < 1e-4
 
 
 @pytest.mark.parametrize("name", ["e2e_batch", "e2e_3s", "e2e_real"])
