@@ -212,10 +212,26 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
   const long long ob = (long long)b * p.y_bstride;
   unsigned short* y6 = p.y6 ? p.y6 + ob * (p.y_compact == 1 ? 1 : p.y_compact == 2 ? 2 : 3) : nullptr;
   unsigned short* y6s = p.y6s ? p.y6s + ob * 3 : nullptr;
-  static_assert(NT % (BN / 4) == 0, "each thread keeps one 4-channel group");
-  const int c4 = (tid % (BN / 4)) * 4, trow = tid / (BN / 4), co = co0 + c4;
-  const f32x4 bias4 = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
-  const f32x4 gamma4 = p.epi == EPI_GAMMA_RES ? *reinterpret_cast<const f32x4*>(p.gamma + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+  // Each thread finishes G consecutive output channels of a row (G = 8: 16-byte plane / compact
+  // stores; the epilogue's store issue, not its bytes, sets its pace), the same channels for every
+  // row, so bias and gamma are loaded once per tile.
+#ifdef DCX_EPI4
+  constexpr int G = 4;  // A/B builds: the round-2 form (8-byte plane stores)
+#else
+  constexpr int G = 8;
+#endif
+  constexpr int NH = G / 4;  // f32x4 halves per thread and row
+  static_assert(NT % (BN / G) == 0, "each thread keeps one channel group");
+  const int cg = (tid % (BN / G)) * G, trow = tid / (BN / G), co = co0 + cg;
+  // LDS read order of the two halves: lanes with bit 3 set read the upper half first, which makes
+  // both ds_read_b128 of a row conflict-free in every 16-lane group (MI355X_MICROARCH.md §LDS)
+  const int hsw = G == 8 ? (lane >> 3) & 1 : 0;
+  f32x4 bias4[NH], gamma4[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    bias4[h] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+    gamma4[h] = p.epi == EPI_GAMMA_RES ? *reinterpret_cast<const f32x4*>(p.gamma + co + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 #ifdef DCX_DIAG_NOEPI
   if (q0 >= 0) return;  // timing-only build: main loop without the epilogue
 #endif
@@ -247,31 +263,34 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
     }
     __syncthreads();
   };
-  // Each thread always finishes the same 4 output channels (NT is a multiple of BN / 4), so bias
-  // and gamma are loaded once per tile.  The residual / mean-accumulator rows of a batch are all
-  // loaded (unconditionally, past-the-end rows clamped) before any of its stores, and the first
-  // batch of a pass before the pass's LDS staging: with stores in flight hipcc can only wait with
-  // vmcnt(0), and conditional loads in a rolled loop made it wait before every single load (one
-  // memory round trip per row).  The stores may alias the loads (the in-place ResBlock state);
-  // each thread stores only elements it has already loaded.
-  constexpr int RSTEP = NT / (BN / 4), ROWS_T = RPP / RSTEP;
+  // The residual / mean-accumulator rows of a batch are all loaded (unconditionally, past-the-end
+  // rows clamped) before any of its stores, and the first batch of a pass before the pass's LDS
+  // staging: with stores in flight hipcc can only wait with vmcnt(0), and conditional loads in a
+  // rolled loop made it wait before every single load (one memory round trip per row).  The stores
+  // may alias the loads (the in-place ResBlock state); each thread stores only elements it has
+  // already loaded.
+  constexpr int RSTEP = NT / (BN / G), ROWS_T = RPP / RSTEP;
   static_assert(RPP % RSTEP == 0, "epilogue rows per thread");
   const bool need_r = p.epi == EPI_GAMMA_RES || p.epi == EPI_RES;
   const bool need_m = p.mean_mode == MEAN_MID || p.mean_mode == MEAN_LAST;
   auto batch = [&](int r0, int rb, bool stage, auto ibt) {
     constexpr int IB = decltype(ibt)::value;
-    f32x4 r[IB], m[IB];
+    f32x4 r[IB][NH], m[IB][NH];
     auto lofs = [&](int k) {
       const int q = min(q0 + r0 + trow + (rb + k) * RSTEP, p.Lq - 1);
       return ob + ((long long)q * p.out_mul + ph) * p.ldy + co;
     };
     if (need_r) {
 #pragma unroll
-      for (int k = 0; k < IB; ++k) r[k] = *reinterpret_cast<const f32x4*>(p.res + lofs(k));
+      for (int k = 0; k < IB; ++k)
+#pragma unroll
+        for (int h = 0; h < NH; ++h) r[k][h] = *reinterpret_cast<const f32x4*>(p.res + lofs(k) + 4 * h);
     }
     if (need_m) {
 #pragma unroll
-      for (int k = 0; k < IB; ++k) m[k] = *reinterpret_cast<const f32x4*>(p.macc + lofs(k));
+      for (int k = 0; k < IB; ++k)
+#pragma unroll
+        for (int h = 0; h < NH; ++h) m[k][h] = *reinterpret_cast<const f32x4*>(p.macc + lofs(k) + 4 * h);
     }
     if (stage) stage_acc(r0);
 #pragma unroll
@@ -281,48 +300,88 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
       if (q >= p.Lq) continue;
       const long long orow = (long long)q * p.out_mul + ph;
       const long long o = ob + orow * p.ldy + co;
-      f32x4 x = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + c4) + bias4;
-      if (p.round_bf16) x = round_bf16x4(x);
-      switch (p.epi) {
-        case EPI_GELU:
+      f32x4 x[NH];
+      if constexpr (NH == 2) {
+        const f32x4 u = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + cg + 4 * hsw);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + cg + 4 * (1 - hsw));
+        x[0] = (hsw ? v : u) + bias4[0];
+        x[1] = (hsw ? u : v) + bias4[1];
+      } else {
+        x[0] = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + cg) + bias4[0];
+      }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) x[e] = p.round_bf16 ? gelu_bf16_f(x[e]) : gelu_f(x[e]);
-          if (p.round_bf16) x = round_bf16x4(x);
-          break;
-        case EPI_GAMMA_RES: x = r[k] + gamma4 * x; break;
-        case EPI_RES: x = r[k] + x; break;
-        case EPI_LOGCLAMP:
+      for (int h = 0; h < NH; ++h) {
+        if (p.round_bf16) x[h] = round_bf16x4(x[h]);
+        switch (p.epi) {
+          case EPI_GELU:
 #pragma unroll
-          for (int e = 0; e < 4; ++e) x[e] = logf(fmaxf(x[e], 1e-5f));
-          break;
-        default: break;
+            for (int e = 0; e < 4; ++e) x[h][e] = p.round_bf16 ? gelu_bf16_f(x[h][e]) : gelu_f(x[h][e]);
+            if (p.round_bf16) x[h] = round_bf16x4(x[h]);
+            break;
+          case EPI_GAMMA_RES: x[h] = r[k][h] + gamma4[h] * x[h]; break;
+          case EPI_RES: x[h] = r[k][h] + x[h]; break;
+          case EPI_LOGCLAMP:
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[h][e] = logf(fmaxf(x[h][e], 1e-5f));
+            break;
+          default: break;
+        }
       }
       if (p.mean_mode == MEAN_FIRST) {
-        *reinterpret_cast<f32x4*>(p.macc + o) = x;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) *reinterpret_cast<f32x4*>(p.macc + o + 4 * h) = x[h];
         continue;
       } else if (p.mean_mode == MEAN_MID) {
-        *reinterpret_cast<f32x4*>(p.macc + o) = m[k] + x;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) *reinterpret_cast<f32x4*>(p.macc + o + 4 * h) = m[k][h] + x[h];
         continue;
       } else if (p.mean_mode == MEAN_LAST) {
-        x = (m[k] + x) / 3.0f;
-      }
-      if (p.y) *reinterpret_cast<f32x4*>(p.y + o) = x;
-      if (y6) {
-        if (p.y_compact == 1) store_bf16x4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
-        else if (p.y_compact == 2) store_hm4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
-        else store_planes4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
-      }
-      if (p.y2 || y6s) {
-        f32x4 sv;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) sv[e] = silu_f(x[e]);
-        if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
-        if (y6s) store_planes4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+        for (int h = 0; h < NH; ++h) x[h] = (m[k][h] + x[h]) / 3.0f;
+      }
+      if (p.y) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h) *reinterpret_cast<f32x4*>(p.y + o + 4 * h) = x[h];
+      }
+      if constexpr (G == 8) {
+        float xv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[e] = x[e >> 2][e & 3];
+        if (y6) {
+          if (p.y_compact == 1) store_bf16x8(y6, orow, p.Cout, co, xv);
+          else if (p.y_compact == 2) store_hm8(y6, orow, p.Cout, co, xv);
+          else store_planes8(y6, orow, p.Cout, co, xv);
+        }
+        if (p.y2 || y6s) {
+          float sv[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sv[e] = silu_f(xv[e]);
+          if (p.y2) {
+            *reinterpret_cast<f32x4*>(p.y2 + o) = f32x4{sv[0], sv[1], sv[2], sv[3]};
+            *reinterpret_cast<f32x4*>(p.y2 + o + 4) = f32x4{sv[4], sv[5], sv[6], sv[7]};
+          }
+          if (y6s) store_planes8(y6s, orow, p.Cout, co, sv);
+        }
+      } else {
+        if (y6) {
+          if (p.y_compact == 1) store_bf16x4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
+          else if (p.y_compact == 2) store_hm4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
+          else store_planes4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
+        }
+        if (p.y2 || y6s) {
+          f32x4 sv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sv[e] = silu_f(x[0][e]);
+          if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
+          if (y6s) store_planes4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+        }
       }
     }
   };
-  // batches of 8 rows (4 when both the residual and the mean accumulator are loaded)
-  constexpr int IBF = ROWS_T < 8 ? ROWS_T : 8, IBM = ROWS_T < 4 ? ROWS_T : 4;
+  // batches of 8 rows (4 when both the residual and the mean accumulator are loaded), halved for
+  // 8-channel groups (the same registers)
+  constexpr int IBF0 = 8 / NH, IBM0 = 4 / NH;
+  constexpr int IBF = ROWS_T < IBF0 ? ROWS_T : IBF0, IBM = ROWS_T < IBM0 ? ROWS_T : IBM0;
   static_assert(ROWS_T % IBF == 0 && ROWS_T % IBM == 0, "epilogue batches");
 #pragma unroll 1
   for (int r0 = 0; r0 < BM; r0 += RPP) {

@@ -87,4 +87,43 @@ __device__ __forceinline__ void store_hm4(unsigned short* base, long long row, i
   *reinterpret_cast<s16x4p*>(dst + 8) = mv;
 }
 
+// 8 consecutive channels c..c+7 (c % 8 == 0) of one row: one 16-byte store per plane.
+typedef short s16x8p __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void store_planes8(unsigned short* base, long long row, int C, int c, const float (&v)[8]) {
+  s16x8p hv, mv, lv;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    unsigned short h, m, l;
+    split3(v[e], h, m, l);
+    hv[e] = (short)h;
+    mv[e] = (short)m;
+    lv[e] = (short)l;
+  }
+  unsigned short* dst = base + plane_off(row, C, c);
+  *reinterpret_cast<s16x8p*>(dst) = hv;
+  *reinterpret_cast<s16x8p*>(dst + 8) = mv;
+  *reinterpret_cast<s16x8p*>(dst + 16) = lv;
+}
+
+__device__ __forceinline__ void store_bf16x8(unsigned short* base, long long row, int C, int c, const float (&v)[8]) {
+  s16x8p hv;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) hv[e] = (short)bf16_bits(v[e]);
+  *reinterpret_cast<s16x8p*>(base + row * (long long)C + c) = hv;
+}
+
+__device__ __forceinline__ void store_hm8(unsigned short* base, long long row, int C, int c, const float (&v)[8]) {
+  s16x8p hv, mv;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    unsigned short h, m, l;
+    split3(v[e], h, m, l);
+    hv[e] = (short)h;
+    mv[e] = (short)m;
+  }
+  unsigned short* dst = base + row * (long long)C * 2 + (c >> 5) * 64 + ((c >> 3) & 3) * 16;
+  *reinterpret_cast<s16x8p*>(dst) = hv;
+  *reinterpret_cast<s16x8p*>(dst + 8) = mv;
+}
+
 }  // namespace dcx
