@@ -2146,6 +2146,7 @@ static hipError_t launch_x6dq(const ConvParams& p, int batch, int phases, hipStr
 // (16-byte unit (r >> 4) * 64 + piece * 16 + (r & 15), piece = 8-channel group of the step).
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
+  DCX_TILET(tile_t0);
   constexpr int BM = 256, BN = 256, WN = 2, WM = 4;
   constexpr int WR = 64, WC = 128, TM = WR / 16, TN = WC / 16;
   constexpr int A_G = BM * 4 / 128, B_G = BN * 4 / 128;  // DMA instructions per group per step
@@ -2237,6 +2238,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
     if (t < nsteps) dma_step(t, t);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   seg_barrier();
+  DCX_TILET(tile_t1);
 #ifdef DCX_CLOCK_DIAG
   const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2277,7 +2279,22 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
     atomicAdd(&g_clock_diag[2], (unsigned long long)(nsteps * 2 / 3));
   }
 #endif
+  DCX_TILET(tile_t2);
   epilogue_lds<BM, BN, WM, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+#ifdef DCX_TILE_DIAG
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+    const unsigned int k = atomicAdd(&g_tile_cnt, 1u);
+    if (k < (unsigned)kTileDiagMax) {
+      unsigned long long* o = g_tile_diag + 6ull * k;
+      o[0] = tile_t0; o[1] = tile_t1; o[2] = tile_t2; o[3] = t3;
+      o[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      o[5] = __builtin_amdgcn_s_getreg((15 << 11) | 20) | ((unsigned long long)nsteps << 16);  // + K32 steps
+    }
+  }
+#endif
 }
 
 // whether conv_gemm_x6dm takes the conv: planes input, Cout % 256, taps >= 2 with a halo or one

@@ -9,7 +9,7 @@ for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY
          "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \
          "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace -d $R/gpurun_out/${TAG}_p$i -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-f32 --no-profile > $R/gpurun_out/${TAG}_p$i.log 2>&1 || { echo "PASS $i failed"; tail -5 $R/gpurun_out/${TAG}_p$i.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace -d $R/gpurun_out/${TAG}_p$i -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-f32 --no-profile --no-c3 --no-c4 --no-c5 --no-oracle-codes > $R/gpurun_out/${TAG}_p$i.log 2>&1 || { echo "PASS $i failed"; tail -5 $R/gpurun_out/${TAG}_p$i.log; exit 1; }
   echo PASS $i ok
 done
 python3 tools/pmc_summary.py $R/gpurun_out/${TAG}_p1 $R/gpurun_out/${TAG}_p2 $R/gpurun_out/${TAG}_p3 > $R/gpurun_out/${TAG}_summary.txt

@@ -23,7 +23,9 @@ from distilcodec_nabeel_amd.engine import NativeConv  # noqa: E402
 
 T = 937
 SHAPES = {"res512_k3": (512, 512, 3, 1, 32, 8 * T), "res512_k11d5": (512, 512, 11, 5, 32, 8 * T),
-          "res256_k7d3": (256, 256, 7, 3, 32, 32 * T), "res128_k3": (128, 128, 3, 1, 32, 64 * T)}
+          "res256_k7d3": (256, 256, 7, 3, 32, 32 * T), "res128_k3": (128, 128, 3, 1, 32, 64 * T),
+          # one round on 120 / 240 of the 256 CUs: the epilogue without the other CUs' bursts
+          "res512_k3_b2": (512, 512, 3, 1, 2, 8 * T), "res512_k3_b4": (512, 512, 3, 1, 4, 8 * T)}
 
 
 def main():
