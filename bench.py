@@ -275,7 +275,7 @@ def run_timed(runner, steps: int, warmup: int, world: int, dev, profile_eng=None
         prof = profile_eng.profile_read()
         profile_eng.profile(False)
     if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device=dev if dist.get_backend() != "gloo" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
         assert all_codes.shape[0] == runner.n_total
@@ -320,9 +320,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DCX_BENCH_ONE_DEVICE=1 (tests/test_gpu_bench_dist.py): rehearse the N > 1 path on a one-GPU box,
+    # every rank on cuda:0 and gloo for the collectives (RCCL refuses two ranks on one device); the
+    # driver's multi-GPU runs use one GPU per rank and RCCL ("nccl")
+    one_dev = os.environ.get("DCX_BENCH_ONE_DEVICE") == "1"
+    if one_dev:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if one_dev:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
     cfg = dconfig.default_config()

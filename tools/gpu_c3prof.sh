@@ -10,4 +10,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $R/gpurun_out/${T
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $R/gpurun_out/${TAG}_write -o run --output-format csv -- python3 tools/c3_bench.py --gemm bf16 --steps 1 > /dev/null 2> $R/gpurun_out/${TAG}_write.err || { echo WRITE_FAILED; exit 1; }
 python3 tools/rocprof_summary.py --stats $(find $R/gpurun_out/${TAG}_trace -name "*kernel_stats.csv" | head -1) --fetch $(find $R/gpurun_out/${TAG}_fetch -name "*counter_collection.csv" | head -1) --write $(find $R/gpurun_out/${TAG}_write -name "*counter_collection.csv" | head -1) --bench-kernels $R/gpurun_out/${TAG}_k_bf16.json > $R/gpurun_out/${TAG}_summary.md
 head -14 $R/gpurun_out/${TAG}_summary.md
-bash tools/gpu_pmc_gen.sh ${TAG}g | tail -60
+[ -n "$SKIP_GEN" ] || bash tools/gpu_pmc_gen.sh ${TAG}g | tail -60
