@@ -156,7 +156,7 @@ def c3_record(cfg, state, dev, steps: int = 3, batch: int = 256):
     kern = eng.profile_read()
     eng.profile(False)
     name, rec = max(kern.items(), key=lambda kv: kv[1]["ms"])
-    prods = 2 if "prefilter_b" in name else 1
+    prods = 1 if "prefilter_b1" in name else 2 if "prefilter_b" in name else 1
     ach = rec["flops"] / (rec["ms"] * 1e-3) / 1e12
     flops = C3_MFLOP_PER_FRAME * 1e6 * batch * T
     out = {"workload": f"C3: encoder + GRFVQ token extraction, {batch} x 10 s, bf16 (enable_bfloat16), codes only",

@@ -104,10 +104,13 @@ struct dcx_codec {
   ConvW vq_down, vq_pin, vq_up;
   BlockW vq_down_blk, vq_up_blk;
   float *codebook = nullptr, *e2 = nullptr, *ptable = nullptr;
+  double* e2d = nullptr;          // |e|^2 per code in fp64 (the rescore)
   float emax = 0.f, e2max = 0.f;  // largest codebook row norm / squared norm (prefilter bound)
+  float dmax = 0.f;               // largest |e - bf16(e)| over the codes (vq_prefilter_b1's bound)
   int* vq_stats = nullptr;        // [rows rescored, codes rescored] (dcx_vq_rescore_stats)
   unsigned short* codebook6 = nullptr;
-  unsigned short* codebook_bk = nullptr;  // hi/mid per K32 step (bf16-mode prefilter, vq_prefilter_bk)
+  unsigned short* codebook_bk = nullptr;  // hi/mid per K32 step (vq_prefilter_bq / _dm; DCX_VQ_OLD builds)
+  unsigned short* codebook_b1 = nullptr;  // [CD/32][NC][32] bf16 hi (vq_prefilter_b1)
   unsigned short* ptable6 = nullptr;  // decode table as activation planes (x6 mode gathers)
   int gemm_mode = DCX_GEMM_X6;
   // fused ResBlock pairs for the C = 32 / 64 generator stages (conv_res_pair); DCX_NO_RESPAIR=1 at
@@ -116,6 +119,9 @@ struct dcx_codec {
   // compact bf16 activations between bf16-mode producers and conv_gemm_bf16dm / vq_prefilter_bk;
   // DCX_NO_COMPACT=1 at dcx_create keeps the planes layout (A/B comparisons, same bits)
   bool compact = true;
+  // rescore candidate-list capacity per searched row (VqScratch); DCX_VQ_PAIRS_PER_ROW at dcx_create
+  // (0: every uncertified row is rescored in place, the overflow path; tests)
+  int vq_pairs_per_row = 64;
   // split-K latency mode (dcx_set_split_k): at most split_k K-slices per few-tile x6 conv; the
   // partial sums live in the first kSplitScratch bytes of each stage call's workspace.  split_buf
   // points there only for the duration of one stage call (CallScope), which `busy` makes exclusive.
@@ -285,6 +291,20 @@ struct Builder {
     if (!bad()) e = {c, m};
   }
 
+  void* upload_raw(const void* src, size_t bytes) {
+    if (bad() || dry) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes + 16) != hipSuccess) {
+      set(DCX_ERR_OOM, "hipMalloc failed while uploading weights");
+      return nullptr;
+    }
+    h->allocs.push_back(p);
+    if (hipMemcpy(p, src, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      set(DCX_ERR_HIP, "hipMemcpy failed while uploading weights");
+      return nullptr;
+    }
+    return p;
+  }
   float* upload(const std::vector<float>& v) {
     if (bad() || dry) return nullptr;
     void* p = nullptr;
@@ -590,8 +610,9 @@ int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32,
   p.x_compact = x6 && c.x.p && c.x.c1 ? 1 : 0;
   p.y_compact = c.y6 ? c.y6c : 0;
   p.wc = one && h->compact ? w.wc : nullptr;
-  if ((p.x_compact == 1 || p.y_compact == 1) && !one)
-    return fail(h, DCX_ERR_STATE, "internal: compact layout outside bf16 mode");
+  // compact inputs only feed one-product GEMMs; a compact output (the RNE hi value) may also be written
+  // in x6 mode (x_pjt_in for vq_prefilter_b1)
+  if (p.x_compact == 1 && !one) return fail(h, DCX_ERR_STATE, "internal: compact layout outside bf16 mode");
   if (p.y_compact == 2 && (!x6 || one)) return fail(h, DCX_ERR_STATE, "internal: hm layout outside x6 mode");
   return DCX_OK;
 }
@@ -825,24 +846,70 @@ int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipSt
   return DCX_OK;
 }
 
+// x_pjt_in layout the nearest-code search reads (ConvParams::x_compact): 1 compact bf16 for
+// vq_prefilter_b1 (x6 and bf16 modes), else 0 planes (vq_prefilter_x3 / _dm; fp32 mode ignores it).
+// DCX_VQ_OLD builds (A/B): 1 in bf16 mode (vq_prefilter_bq), 2 "hm" in x6 mode (vq_prefilter_dm).
+int vq_xlayout(const dcx_codec* h, long long M) {
+  if (!x6_mode(h) || !h->compact) return 0;
+#ifdef DCX_VQ_OLD
+  if (!h->codebook_bk) return 0;
+  if (h->gemm_mode == DCX_GEMM_BF16) return 1;
+  return dcx::vq_hm_takes(h->cfg.codebook_size, h->cfg.codebook_dim, M) ? 2 : 0;
+#else
+  (void)M;
+  return h->codebook_b1 ? 1 : 0;
+#endif
+}
+
 // The nearest-code search of DownsampleGRVQ (vector_quantize_pytorch.py:41-45, 496-506; first index on
 // ties) on x_pjt_in P (fp32 [M][CD]) and, in x6 / bf16 mode, P6 in the prefilter's layout xl (0 planes,
 // 1 compact bf16, 2 hm): |x|^2, the certified prefilter and the fp64 rescore (x6 / bf16), or the exact
 // fp32 distance GEMM and its reduce (fp32 mode).  pv / pi / pv2: [M][ntiles] scratch, x2: [M].
-int run_vq_search(dcx_codec* h, const float* P, const unsigned short* P6, int xl, long long M, float* x2, float* pv,
-                  int* pi, float* pv2, int ntiles, int32_t* codes, hipStream_t s) {
+// Workspace of one search of M rows: the prefilter's [M][ntiles] partials and, in x6 / bf16 mode, the
+// rescore's candidate list (64 pairs per row on average; a row that does not fit is rescored in place).
+struct VqScratch {
+  float *x2 = nullptr, *xr2 = nullptr, *pv = nullptr, *pv2 = nullptr;
+  int* pi = nullptr;
+  double *x2d = nullptr, *dist = nullptr;
+  int2 *pairs = nullptr, *row_list = nullptr;
+  unsigned long long* npairs = nullptr;
+  long long cap = 0;
+};
+VqScratch vq_scratch(const dcx_codec* h, Bump& ws, long long M, int ntiles, bool x6) {
+  VqScratch v;
+  v.x2 = ws.f((size_t)M);
+  v.pv = ws.f((size_t)M * ntiles);
+  v.pi = ws.i((size_t)M * ntiles);
+  if (x6) {
+    v.xr2 = ws.f((size_t)M);
+    v.pv2 = ws.f((size_t)M * ntiles);
+    v.x2d = (double*)ws.raw((size_t)M * sizeof(double));
+    v.cap = h->vq_pairs_per_row > 0 ? std::max<long long>((long long)h->vq_pairs_per_row * M, 1024) : 0;
+    v.pairs = (int2*)ws.raw((size_t)v.cap * sizeof(int2));
+    v.dist = (double*)ws.raw((size_t)v.cap * sizeof(double));
+    v.row_list = (int2*)ws.raw((size_t)M * sizeof(int2));
+    v.npairs = (unsigned long long*)ws.raw(sizeof(unsigned long long));
+  }
+  return v;
+}
+
+int run_vq_search(dcx_codec* h, const float* P, const unsigned short* P6, int xl, long long M, const VqScratch& v,
+                  int ntiles, int32_t* codes, hipStream_t s) {
   const dcx_config& c = h->cfg;
   const int CD = c.codebook_dim, NC = c.codebook_size;
   const bool x6 = x6_mode(h);
   const bool p6c = xl == 1, p6hm = xl == 2;
-  LAUNCH(h, s, "row_sqnorm", 2.0 * M * CD, 4.0 * M * CD, dcx::launch_row_sqnorm(P, M, CD, x2, s));
+  const bool b1 = p6c && dcx::vq_b1_takes(NC, CD);
+  float* const x2 = v.x2;
+  LAUNCH(h, s, "row_sqnorm", 2.0 * M * CD, 4.0 * M * CD,
+         dcx::launch_row_sqnorm(P, M, CD, x2, x6 ? v.x2d : nullptr, b1 ? v.xr2 : nullptr, x6 ? v.npairs : nullptr, s));
   {
     ConvParams p{};
     p.x = P; p.x6 = P6; p.w = h->codebook; p.w6 = x6 ? h->codebook6 : nullptr;
     p.Cin = CD; p.Cout = NC; p.ldx = CD; p.taps = 1; p.in_step = 1; p.out_mul = 1;
-    p.x2 = x2; p.e2 = h->e2; p.part_val = pv; p.part_idx = pi; p.part_val2 = pv2;
+    p.x2 = x2; p.e2 = h->e2; p.part_val = v.pv; p.part_idx = v.pi; p.part_val2 = v.pv2;
     p.x_compact = p6c ? 1 : p6hm ? 2 : 0;
-    p.wc = p6c || p6hm ? h->codebook_bk : nullptr;
+    p.wc = b1 ? h->codebook_b1 : p6c || p6hm ? h->codebook_bk : nullptr;
     ProfScope ps(h, s);
     const char* kname = "vq";
     if (x6) {
@@ -854,12 +921,19 @@ int run_vq_search(dcx_codec* h, const float* P, const unsigned short* P6, int xl
       ps.done(kname, 2.0 * M * NC * CD, 4.0 * ((double)M * CD + (double)NC * CD));
     }
   }
-  if (x6)
-    LAUNCH(h, s, "vq_rescore", 0, 12.0 * M * ntiles + 4.0 * M,
-           dcx::launch_vq_rescore(pv, pi, pv2, M, ntiles, NC / ntiles, P, x2, CD, h->codebook, h->emax, h->e2max,
-                                  dcx::kVqPrefilterBound, codes, h->vq_stats, s));
-  else
-    LAUNCH(h, s, "vq_reduce", 0, 8.0 * M * ntiles, dcx::launch_vq_reduce(pv, pi, (int)M, ntiles, codes, s));
+  if (x6) {
+    dcx::VqRescoreArgs a{};
+    a.part_val = v.pv; a.part_val2 = v.pv2; a.part_idx = v.pi;
+    a.rows = M; a.ntiles = ntiles; a.tile_codes = NC / ntiles; a.dim = CD;
+    a.x = P; a.x2 = x2; a.xr2 = b1 ? v.xr2 : nullptr; a.x2d = v.x2d;
+    a.codebook = h->codebook; a.e2d = h->e2d;
+    a.cx = dcx::vq_prefilter_cx(xl, NC, CD, h->emax, h->dmax); a.emax = h->emax; a.e2max = h->e2max;
+    a.codes = codes; a.stats = h->vq_stats;
+    a.pairs = v.pairs; a.dist = v.dist; a.cap = v.cap; a.row_list = v.row_list; a.npairs = v.npairs;
+    LAUNCH(h, s, "vq_rescore", 0, 12.0 * M * ntiles + 4.0 * M, dcx::launch_vq_rescore(a, s));
+  } else {
+    LAUNCH(h, s, "vq_reduce", 0, 8.0 * M * ntiles, dcx::launch_vq_reduce(v.pv, v.pi, (int)M, ntiles, codes, s));
+  }
   return DCX_OK;
 }
 
@@ -869,11 +943,8 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   const long long M = (long long)B * T;
   const int D = c.vq_dim, CD = c.codebook_dim, NC = c.codebook_size;
   const bool x6 = x6_mode(h);
-  // x_pjt_in layout for the prefilter: compact bf16 (bf16 mode, vq_prefilter_bk), "hm" (x6 mode,
-  // vq_prefilter_dm, more than one row panel) or planes
-  const bool p6c = x6 && h->compact && h->gemm_mode == DCX_GEMM_BF16 && h->codebook_bk;
-  const bool p6hm = x6 && h->compact && h->gemm_mode == DCX_GEMM_X6 && h->codebook_bk && dcx::vq_hm_takes(NC, CD, M);
-  const int ntiles = x6 ? dcx::vq_prefilter_ntiles(NC, CD, M, p6c ? 1 : p6hm ? 2 : 0) : dcx::vq_argmin_ntiles(NC);
+  const int xl = vq_xlayout(h, M);
+  const int ntiles = x6 ? dcx::vq_prefilter_ntiles(NC, CD, M, xl) : dcx::vq_argmin_ntiles(NC);
   RUN(ensure_planes(h, feat, M, D, ws, s, takes_compact(h, h->vq_down, M)));
   if (feat.c1 && !takes_compact(h, h->vq_down, M)) return fail(h, DCX_ERR_STATE, "internal: compact features");
   float* X = ws.f((size_t)M * D);
@@ -882,10 +953,7 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   Act hid = conv_input(h, ws, (size_t)M * 4 * D);
   float* P = pin ? pin : ws.f((size_t)M * CD);
   unsigned short* P6 = x6 ? ws.u16((size_t)M * CD * 3) : nullptr;
-  float* x2 = ws.f((size_t)M);
-  float* pv = ws.f((size_t)M * ntiles);
-  int* pi = ws.i((size_t)M * ntiles);
-  float* pv2 = x6 ? ws.f((size_t)M * ntiles) : nullptr;
+  const VqScratch vs = vq_scratch(h, ws, M, ntiles, x6);
   Act zd = conv_input(h, ws, (size_t)M * D);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for vq_encode");
@@ -893,14 +961,13 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   cd.y = X;
   RUN(run_conv(h, h->vq_down, cd, s));
   const bool x6c = X6 && takes_compact(h, h->vq_pin, M);
-  // bf16 mode: x_pjt_in compact for vq_prefilter_bk (the repacked codebook exists iff it takes the shape)
   RUN(run_block(h, h->vq_down_blk, X, X6, B, T, ln, hid, s, x6c));
   ConvCall cp = pointwise(CAct(X, X6, x6c), M);
   cp.y = P;
   cp.y6 = P6;
-  cp.y6c = p6c ? 1 : p6hm ? 2 : 0;
+  cp.y6c = xl;
   RUN(run_conv(h, h->vq_pin, cp, s));
-  RUN(run_vq_search(h, P, P6, p6c ? 1 : p6hm ? 2 : 0, M, x2, pv, pi, pv2, ntiles, codes, s));
+  RUN(run_vq_search(h, P, P6, xl, M, vs, ntiles, codes, s));
   if (fup) LAUNCH(h, s, "gather_rows", 0, 8.0 * M * CD, dcx::launch_gather_rows(h->codebook, NC, codes, M, CD, fup, nullptr, -1, s));
   if (quant) {
     if (x6)
@@ -1217,17 +1284,14 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
     const int CD = c.codebook_dim, NC = c.codebook_size;
     if (h->gemm_mode == DCX_GEMM_BF16) return fail(h, DCX_ERR_INVALID_ARG, "quantizer.search takes x6 or fp32 arithmetic");
     const bool x6 = x6_mode(h);
-    const bool hm = x6 && h->compact && h->codebook_bk && dcx::vq_hm_takes(NC, CD, M);
-    const int ntiles = x6 ? dcx::vq_prefilter_ntiles(NC, CD, M, hm ? 2 : 0) : dcx::vq_argmin_ntiles(NC);
+    const int xl = vq_xlayout(h, M);
+    const int ntiles = x6 ? dcx::vq_prefilter_ntiles(NC, CD, M, xl) : dcx::vq_argmin_ntiles(NC);
     unsigned short* P6 = x6 ? ws.u16((size_t)M * CD * 3) : nullptr;
-    float* x2 = ws.f((size_t)M);
-    float* pv = ws.f((size_t)M * ntiles);
-    int* pi = ws.i((size_t)M * ntiles);
-    float* pv2 = x6 ? ws.f((size_t)M * ntiles) : nullptr;
+    const VqScratch vs = vq_scratch(h, ws, M, ntiles, x6);
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
-    if (x6) LAUNCH(h, s, "split_planes", 0, 10.0 * M * CD, dcx::launch_split_planes(x, P6, M, CD, hm ? 2 : 0, s));
-    return run_vq_search(h, x, P6, hm ? 2 : 0, M, x2, pv, pi, pv2, ntiles, static_cast<int32_t*>(yv), s);
+    if (x6) LAUNCH(h, s, "split_planes", 0, 10.0 * M * CD, dcx::launch_split_planes(x, P6, M, CD, xl, s));
+    return run_vq_search(h, x, P6, xl, M, vs, ntiles, static_cast<int32_t*>(yv), s);
   }
   if (!h->has_gen && m.rfind("generator.", 0) == 0) return fail(h, DCX_ERR_STATE, "generator weights were not finalized");
   // ConvTranspose1d (generators.py:118-147, ups[i])
@@ -1390,6 +1454,8 @@ int dcx_create(const dcx_config* cfg, dcx_codec** out) {
   h->res_pair = !(nrp && nrp[0] == '1');
   const char* ncp = std::getenv("DCX_NO_COMPACT");
   h->compact = !(ncp && ncp[0] == '1');
+  const char* vpr = std::getenv("DCX_VQ_PAIRS_PER_ROW");
+  if (vpr && vpr[0]) h->vq_pairs_per_row = std::max(0, std::atoi(vpr));
   *out = h;
   return DCX_OK;
 }
@@ -1469,13 +1535,16 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
     auto emb = B.need(q + "grvq.rvqs.0.layers.0._codebook.embed", {1, NC, CD});
     if (emb) {
       std::vector<float> e2(NC);
+      std::vector<double> e2d(NC);
       double e2m = 0;
       for (int i = 0; i < NC; ++i) {
         double sacc = 0;
         for (int d = 0; d < CD; ++d) sacc += (double)emb->data[(size_t)i * CD + d] * emb->data[(size_t)i * CD + d];
         e2[i] = (float)sacc;
+        e2d[i] = sacc;
         e2m = std::max(e2m, sacc);
       }
+      h->e2d = (double*)B.upload_raw(e2d.data(), e2d.size() * sizeof(double));
       // rounded up so the prefilter bound stays an upper bound
       h->e2max = std::nextafter((float)e2m, INFINITY);
       h->emax = std::nextafter((float)std::sqrt(e2m), INFINITY);
@@ -1483,6 +1552,20 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
       h->codebook = B.upload(emb->data);
       h->codebook6 = B.split_pack(emb->data, 1, NC, 1, CD);
       h->e2 = B.upload(e2);
+      // max |e - bf16(e)| in fp64, rounded up (vq_prefilter_b1's bound)
+      double d2m = 0;
+      for (int i = 0; i < NC; ++i) {
+        double sacc = 0;
+        for (int d = 0; d < CD; ++d) {
+          const float v = emb->data[(size_t)i * CD + d];
+          const double r = (double)v - (double)bf16_f(bf16_rne(v));
+          sacc += r * r;
+        }
+        d2m = std::max(d2m, sacc);
+      }
+      h->dmax = std::nextafter((float)(std::sqrt(d2m) * (1.0 + 1e-12)), INFINITY);
+      if (dcx::vq_b1_takes(NC, CD)) h->codebook_b1 = B.compact_pack(emb->data, NC, CD);
+#ifdef DCX_VQ_OLD
       if (dcx::vq_bk_takes(NC, CD)) {
         h->codebook_bk = (unsigned short*)B.alloc((size_t)NC * CD);  // NC * CD * 2 bf16 (hi, mid)
         if (!B.bad() && !B.dry &&
@@ -1490,6 +1573,7 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
              hipDeviceSynchronize() != hipSuccess))
           return fail(h, DCX_ERR_HIP, "bf16 codebook repack failed");
       }
+#endif
     }
     // decode table: project_out applied to every code once, E * W_out^T + b_out.  Row NC holds
     // project_out(0) = b_out, the row of the reference's masked code -1 (residual_vq.py:120-127:

@@ -1639,6 +1639,8 @@ __device__ __forceinline__ void wait_dma(int n) {  // n = DMA pieces this wave i
   case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
   switch (n) {
     DCX_W(1) DCX_W(2) DCX_W(3) DCX_W(4) DCX_W(5) DCX_W(6) DCX_W(7) DCX_W(8) DCX_W(9) DCX_W(10) DCX_W(11)
+    DCX_W(12) DCX_W(13) DCX_W(14) DCX_W(15) DCX_W(16) DCX_W(17) DCX_W(18) DCX_W(19) DCX_W(20) DCX_W(21) DCX_W(22)
+    DCX_W(23)
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 #undef DCX_W
@@ -3061,6 +3063,151 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_bq(const ConvParams p) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// vq_prefilter_b1: one bf16 product per term, x_h . e_h', in both arithmetic modes (round 3).
+//
+// The search only needs a candidate set that provably holds the nearest code; vq_rescore_kernel
+// settles it exactly in fp64.  With x = x_h + x_r and e = e_h + d (x_h, e_h the RNE bf16 values),
+// x.e - x_h.e_h = x_r.e + x_h.d, so by Cauchy-Schwarz the dropped terms are at most
+// |x_r| max|e| + |x_h| max|d|, where max|d| (0.17 % of max|e| on the synthetic codebook) is
+// measured once at load and |x_r| per row by row_sqnorm (zero in bf16 mode).  That bound is
+// looser than vq_prefilter_dm's (3 products) or vq_prefilter_bq's (2), so more rows go on to the
+// rescore (about 60-95 % instead of 10 %, 3-7 candidates each), but the distance GEMM, 99 % of the
+// search's MFMA work, issues 1/3 (x6) or 1/2 (bf16) of the products.
+//
+// One v_mfma_f32_16x16x32_bf16 per 16 x 16 block and K32 step (lanes l >> 4 = 0..3 read the four
+// 16-byte pieces of 8 channels).  Both operands arrive as 64-byte runs per row / code and step:
+// x_pjt_in compact ([rows][CD] bf16, the project_in epilogue's y_compact == 1 output) and the
+// codebook as launch_repack_codebook_b1 packs it ([CD/32][NC][32] bf16).  LDS images: 64-byte
+// rows, piece q in slot q ^ ((row >> 2) & 3) (vq_prefilter_bk's x image), conflict-free for the
+// four lane groups of a ds_read_b128.  Ring: NS slots of 16 + 16 KiB on the ping-pong schedule
+// of vq_prefilter_bk generalised to NS slots: step t is issued by group 0 in MEM0(t - NS) and by
+// group 1 in MEM1(t - NS + 1), and each wave retires its pieces NS - 2 memory segments later.
+// ---------------------------------------------------------------------------------------------
+template <int NS>
+__global__ void __launch_bounds__(512, 2) vq_prefilter_b1(const ConvParams p) {
+  constexpr int BM = 256, BN = 256, WN = 2;
+  constexpr int WR = BM / 4, WC = BN / 2, TM = WR / 16, TN = WC / 16;
+  constexpr int RW = 32;                       // ushorts per LDS row (64 bytes)
+  constexpr int A_G = BM * 4 / 64 / 2;         // DMA instructions per group per tile (8)
+  constexpr int B_G = BN * 4 / 64 / 2;         // (8)
+  constexpr int A_PW = A_G / 4, B_PW = B_G / 4;  // per wave (2 + 2)
+  constexpr int P = A_PW + B_PW;
+  constexpr int ABUF = BM * RW, BBUF = BN * RW;
+  constexpr int LDS_US = NS * (ABUF + BBUF);   // NS * 32 KiB
+  static_assert(A_G % 4 == 0 && B_G % 4 == 0 && LDS_US * 2 <= 160 * 1024 && NS >= 3, "tile shape");
+  static_assert(P * (NS - 1) <= 23, "wait_dma range");
+  __shared__ __attribute__((aligned(16))) unsigned short lds[LDS_US];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int group = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntiles = p.Cout / BN, mtiles = (p.Lq + BM - 1) / BM;
+  int mt, nt;
+  vq_tile(mtiles, ntiles, mt, nt);
+  if (mt >= mtiles) return;  // whole workgroup, before any barrier
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int nsteps = p.Cin / 32;
+  const int arow = p.ldx * 2;  // bytes per compact row
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.x6 + (long long)q0 * p.ldx), 0, min(BM, p.Lq - q0) * arow, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wc, 0, nsteps * p.Cout * 64, 0x00020000);
+
+  int a_off[A_PW], b_off[B_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int u = (group * A_G + i * 4 + gw) * 64 + lane;
+    const int row = u >> 2, pc = (u & 3) ^ ((row >> 2) & 3);
+    a_off[i] = row * arow + pc * 16;
+  }
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int u = (group * B_G + i * 4 + gw) * 64 + lane;
+    const int code = u >> 2, pc = (u & 3) ^ ((code >> 2) & 3);
+    b_off[i] = (co0 + code) * 64 + pc * 16;
+  }
+  unsigned short* const a_dst = lds + (group * A_G + gw) * 512;
+  unsigned short* const b_dst = lds + NS * ABUF + (group * B_G + gw) * 512;
+  auto dma_step = [&](int c, int slot) {
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) dma16(rx, a_dst + slot * ABUF + i * 2048, a_off[i] + c * 64, 0);
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) dma16(rw, b_dst + slot * BBUF + i * 2048, b_off[i], c * p.Cout * 64);
+  };
+
+  // lane roles: row / code l & 15 of a 16-block, piece (8 channels) q = l >> 4
+  const int l16 = lane & 15, pq = lane >> 4;
+  s16x8 af[TM], bfr[TN];
+  auto readF = [&](int slot) {
+    const unsigned short* A = lds + slot * ABUF;
+    const unsigned short* Bs = lds + NS * ABUF + slot * BBUF;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm * WR + i * 16 + l16;
+      af[i] = *reinterpret_cast<const s16x8*>(A + r * RW + ((pq ^ ((r >> 2) & 3)) << 3));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WC + j * 16 + l16;
+      bfr[j] = *reinterpret_cast<const s16x8*>(Bs + col * RW + ((pq ^ ((col >> 2) & 3)) << 3));
+    }
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                            __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto inc = [](int& slot) { slot = slot == NS - 1 ? 0 : slot + 1; };
+  // pieces this wave may leave in flight at the end of a memory segment: its shares of the steps
+  // after the ones the next two segments read (lo..hi inclusive, clipped to the steps that exist)
+  auto in_flight = [&](int lo, int hi) { return P * max(0, min(hi, nsteps - 1) - lo + 1); };
+
+  for (int t = 0; t < NS && t < nsteps; ++t) dma_step(t, t);
+  // group 0 reads step 0 now and step 1 in segment 1 (its own MFMA segment 0 comes first)
+  wait_dma(group == 0 ? in_flight(2, NS - 1) : in_flight(1, NS - 1));
+  seg_barrier();
+  if (group == 0) {
+    readF(0);
+    int rs = 1, ws = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      mfma();  // MFMA(s)
+      seg_barrier();
+      if (s + 1 < nsteps) readF(rs);  // MEM0(s): fragments of step s + 1, issue step s + NS
+      if (s + NS < nsteps) dma_step(s + NS, ws);
+      wait_dma(in_flight(s + 3, s + NS));
+      seg_barrier();
+      inc(rs);
+      inc(ws);
+    }
+  } else {
+    int rs = 0, ws = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      readF(rs);  // MEM1(s): fragments of step s, issue step s + NS - 1 (s >= 1)
+      if (s >= 1 && s + NS - 1 < nsteps) dma_step(s + NS - 1, ws);
+      wait_dma(in_flight(s + 2, s >= 1 ? s + NS - 1 : NS - 1));
+      seg_barrier();
+      mfma();  // MFMA(s)
+      seg_barrier();
+      inc(rs);
+      if (s >= 1) inc(ws);
+      else ws = 0;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  epilogue_top2_q<BM, BN, 4, WN>(p, acc, q0, co0, nt, ntiles, reinterpret_cast<float*>(lds));
+}
+
+// ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, bool ARGMIN>
@@ -3328,13 +3475,47 @@ bool vq_hm_takes(int ncodes, int dim, long long rows) {
   return vq_bk_takes(ncodes, dim) && vq_dm_ok(ncodes, dim);
 }
 
+// vq_prefilter_b1's ring depth (slots of 32 KiB; DCX_VQ_NS=3..5 in A/B builds)
+#ifndef DCX_VQ_NS
+#define DCX_VQ_NS 4
+#endif
+bool vq_b1_takes(int ncodes, int dim) {
+#ifdef DCX_VQ_OLD
+  return false;
+#endif
+  return ncodes % (256 * 16) == 0 && dim % 32 == 0 && dim / 32 >= DCX_VQ_NS && (long long)dim * 2 * 256 < (1ll << 31) &&
+         (long long)(dim / 32) * ncodes * 64 < (1ll << 31);
+}
+
+// vq_prefilter_b1 (x_layout 1 unless built with DCX_VQ_OLD): x.e - x_h.e_h = x_r.e + x_h.d with
+// |x_r.e| <= |x_r| max|e| (the rescore's second term) and |x_h.d| <= |x_h| max|d| <= (1 + 2^-8)|x| dmax;
+// fp32 summation of the dim exact products, in whatever order the MFMAs add them, errs by at most
+// dim 2^-24 sum_k |x_h,k e_h,k| <= dim 2^-24 (1 + 2^-8)^2 |x| max|e|.  The other kernels: the
+// kVqPrefilterBound form of the comment above vq_bk_takes.
+double vq_prefilter_cx(int x_layout, int ncodes, int dim, float emax, float dmax) {
+  if (x_layout != 1 || !vq_b1_takes(ncodes, dim)) return (double)kVqPrefilterBound * emax;
+  return (1.0 + 0x1p-8) * (double)dmax + (double)dim * 0x1p-24 * (1.0 + 0x1p-6) * (double)emax;
+}
+
 hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipStream_t s, const char** kname) {
   constexpr int BM = 256, BN = 128;
-  if (!p.w6 || !p.x6 || !p.part_val2 || p.Cin % BK || p.Cout % (BN * 16) || rows < 1) return hipErrorInvalidValue;
+  if (!p.x6 || !p.part_val2 || rows < 1) return hipErrorInvalidValue;
   ConvParams q = p;
   q.Lq = rows;
   q.Lin = rows;
   q.taps = 1;
+#ifndef DCX_VQ_OLD
+  if (p.x_compact == 1) {  // compact x_pjt_in (either mode) and the [CD/32][NC][32] hi codebook
+    if (!p.wc || !vq_b1_takes(p.Cout, p.Cin)) return hipErrorInvalidValue;
+    const int mtiles = (rows + 255) / 256, ntiles = p.Cout / 256;
+    const dim3 grid(vq_grid(mtiles, ntiles));
+    if (kname) *kname = "vq_prefilter_b1<256,256>";
+    hipLaunchKernelGGL(vq_prefilter_b1<DCX_VQ_NS>, grid, dim3(512), 0, s, q);
+    return hipGetLastError();
+  }
+  if (p.x_compact == 2) return hipErrorInvalidValue;
+#endif
+  if (!p.w6 || p.Cin % BK || p.Cout % (BN * 16)) return hipErrorInvalidValue;
   if (p.x_compact == 2) {  // x6 mode, "hm" x_pjt_in and the repacked codebook: vq_prefilter_dm
     if (x_bf16 || !p.wc || !vq_hm_takes(p.Cout, p.Cin, rows)) return hipErrorInvalidValue;
     const int mtiles = (rows + 255) / 256, ntiles = p.Cout / 256;

@@ -123,17 +123,47 @@ int vq_prefilter_ntiles(int ncodes, int dim, long long rows, int x_layout);
 // x_bf16: the rows of x are bf16 values (mid and lo planes zero), which drops the mid*hi product.
 // p.x_compact == 1 (bf16 mode) / 2 (x6 mode, "hm" layout) with p.wc the launch_repack_codebook_bk
 // codebook: vq_prefilter_bk / vq_prefilter_dm reading contiguous runs.
+// p.x_compact == 1 with p.wc the [CD/32][NC][32] bf16 hi codebook: vq_prefilter_b1 (one product,
+// both modes; vq_b1_takes).  Built with -DDCX_VQ_OLD (A/B): p.x_compact == 1 (bf16 mode) / 2 (x6
+// mode, "hm" layout) with p.wc the launch_repack_codebook_bk codebook: vq_prefilter_bq / _dm.
 hipError_t launch_vq_prefilter(const ConvParams& p, int rows, bool x_bf16, hipStream_t s, const char** kname);
+bool vq_b1_takes(int ncodes, int dim);
 // ... then per row: certify the prefilter's winner with a rigorous error bound, or rescore every
 // candidate inside the bound in fp64.  stats (optional): [0] rows rescored, [1] codes rescored.
 constexpr float kVqPrefilterBound = 2.5e-4f;
-hipError_t launch_vq_rescore(const float* part_val, const int* part_idx, const float* part_val2, long long rows,
-                             int ntiles, int tile_codes, const float* x, const float* x2, int dim,
-                             const float* codebook, float emax, float e2max, float cbound, int32_t* codes, int* stats,
-                             hipStream_t s);
+// Coefficient cx of |x| in the half-width of the prefilter's error for x_pjt_in in layout x_layout
+// (vq_rescore: bound = 2 (cx |x| + max|e| |x_r|) + 8 2^-24 (|x|^2 + max|e|^2)); dmax = max |e - bf16(e)|.
+double vq_prefilter_cx(int x_layout, int ncodes, int dim, float emax, float dmax);
+// vq_rescore arguments.  part_*: the prefilter's [rows][ntiles] partials; x: x_pjt_in fp32
+// [rows][dim]; x2 / x2d: |x|^2 per row (row_sqnorm, fp32 / fp64); xr2 (optional): |x - bf16(x)|^2,
+// required for vq_prefilter_b1's bound; e2d: |e|^2 per code in fp64; cx / emax / e2max: the bound
+// (vq_prefilter_cx).  Workspace: pairs / dist [cap] candidate list, row_list [rows], npairs (zeroed
+// by row_sqnorm before the prefilter).  stats (optional): [0] rows rescored, [1] codes rescored.
+struct VqRescoreArgs {
+  const float *part_val, *part_val2;
+  const int* part_idx;
+  long long rows;
+  int ntiles, tile_codes, dim;
+  const float *x, *x2, *xr2;
+  const double* x2d;
+  const float* codebook;
+  const double* e2d;
+  double cx;
+  float emax, e2max;
+  int32_t* codes;
+  int* stats;
+  int2* pairs;
+  double* dist;
+  long long cap;
+  int2* row_list;
+  unsigned long long* npairs;
+};
+hipError_t launch_vq_rescore(const VqRescoreArgs& a, hipStream_t s);
 hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows, int ntiles, int32_t* codes,
                             hipStream_t s);
-hipError_t launch_row_sqnorm(const float* x, long long rows, int C, float* out, hipStream_t s);
+// x2 (fp32) and optionally x2d (fp64) |x|^2, xr2 |x - bf16(x)|^2 per row; zero_me (optional) set to 0
+hipError_t launch_row_sqnorm(const float* x, long long rows, int C, float* out, double* x2d, float* xr2,
+                             unsigned long long* zero_me, hipStream_t s);
 // y6c: y6 in the compact bf16 layout instead of planes
 hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, int y6c, const float* w, const float* b,
                           long long rows, int C, float eps, int channels_first_form, hipStream_t s);

@@ -5,6 +5,8 @@
 #include "dcx_kernels.h"
 #include "dcx_planes.h"
 
+#include <algorithm>
+
 namespace dcx {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -292,25 +294,44 @@ hipError_t launch_split_planes(const float* x, unsigned short* y6, long long row
 // ---------------------------------------------------------------------------------------------
 // VQ helpers
 // ---------------------------------------------------------------------------------------------
-// |x|^2 per row (vector_quantize_pytorch.py:42), accumulated in fp64 and rounded once.
+// |x|^2 per row (vector_quantize_pytorch.py:42), accumulated in fp64: rounded once to fp32 (out,
+// the prefilter's epilogue) and kept in fp64 (x2d, the rescore).  With xr2, also |x - bf16(x)|^2
+// (the residual the one-product prefilter vq_prefilter_b1 drops from x).  Thread 0 also zeroes the
+// rescore's pair counter (zero_me), so the search issues no memset node when graph-captured.
 __global__ void __launch_bounds__(256) row_sqnorm_kernel(const float* __restrict__ x, long long rows, int C,
-                                                          float* __restrict__ out) {
+                                                          float* __restrict__ out, double* __restrict__ x2d,
+                                                          float* __restrict__ xr2, unsigned long long* __restrict__ zero_me) {
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (zero_me && blockIdx.x == 0 && threadIdx.x == 0) *zero_me = 0;
   if (row >= rows) return;
-  double s = 0.0;
+  double s = 0.0, r = 0.0;
   for (int c = lane * 4; c < C; c += 256) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(x + row * C + c);
     s += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double d = (double)v[k] - (double)bf16_val(bf16_bits(v[k]));
+      r += d * d;
+    }
   }
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (lane == 0) out[row] = (float)s;
+  for (int off = 32; off >= 1; off >>= 1) {
+    s += __shfl_xor(s, off, 64);
+    r += __shfl_xor(r, off, 64);
+  }
+  if (lane == 0) {
+    out[row] = (float)s;
+    if (x2d) x2d[row] = s;
+    if (xr2) xr2[row] = (float)r;
+  }
 }
 
-hipError_t launch_row_sqnorm(const float* x, long long rows, int C, float* out, hipStream_t s) {
+hipError_t launch_row_sqnorm(const float* x, long long rows, int C, float* out, double* x2d, float* xr2,
+                             unsigned long long* zero_me, hipStream_t s) {
   if (C % 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(row_sqnorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, rows, C, out);
+  hipLaunchKernelGGL(row_sqnorm_kernel, dim3((unsigned)std::max<long long>((rows + 3) / 4, 1)), dim3(256), 0, s, x,
+                     rows, C, out, x2d, xr2, zero_me);
   return hipGetLastError();
 }
 
@@ -343,13 +364,25 @@ hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows
   return hipGetLastError();
 }
 
-// VQ search, second half (x6 mode): one workgroup per row.  From the prefilter's per-tile
-// (smallest, second smallest, code of smallest) approximate squared distances:
-//   best = smallest approximate value; thr = best + 2 * bound (launch_vq_prefilter's bound);
+// VQ search, second half (x6 and bf16 modes).  From the prefilter's per-tile (smallest, second
+// smallest, code of smallest) approximate squared distances of a row:
+//   best = smallest approximate value; thr = best + 2 * bound (vq_prefilter_cx's bound);
 //   a tile is a candidate if its smallest <= thr, and wholly a candidate if its second <= thr.
 // One candidate code: it is the exact argmin; done.  Otherwise every candidate code is rescored
 // with an fp64 dot product and fp64 norms, smallest exact distance, lowest index on ties (the
 // reference's first-index argmax of -dist).
+//
+// Three launches (round 3), because with the one-product prefilter most rows have 2-10 candidates
+// (up to whole 256-code tiles in x6 mode), and evaluating them serially per row left the rescore
+// latency-bound (one workgroup per row: 9.9 ms at C3, 4.3 ms at C2):
+//   vq_certify_kernel    one wave per row: certifies, or reserves a contiguous block of
+//                        (row, code) pairs in the workspace list (a vector atomicAdd on one
+//                        counter) and writes the row's candidates there in tile order;
+//   vq_pair_eval_kernel  one wave per pair: d = (|x|^2 + |e|^2) - 2 x.e in fp64 (|x|^2 and |e|^2
+//                        the fp64 sums of row_sqnorm and of the load-time codebook pass);
+//   vq_pair_reduce_kernel one wave per listed row: smallest d, lowest code on exact ties.
+// A row whose candidates would overflow the list is rescored by its own wave in the certify
+// kernel (the same fp64 arithmetic), so the result never depends on the list capacity.
 constexpr int kMaxVqTiles = 512;
 constexpr int kMaxVqDimVec = 16;  // dim <= 16 * 256
 
@@ -358,136 +391,185 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
+__device__ __forceinline__ bool dless(double d, int c, double bd, int bc) { return d < bd || (d == bd && c < bc); }
 
-__global__ void __launch_bounds__(256) vq_rescore_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
+// x.e in fp64 over one wave (lane-strided float4s; every lane returns the sum)
+__device__ __forceinline__ double dot_f64(const float* __restrict__ xrow, const float* __restrict__ crow, int nvec,
+                                          int lane) {
+  double acc = 0;
+#pragma unroll 7
+  for (int u = 0; u < nvec; ++u) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(xrow + u * 256 + lane * 4);
+    const f32x4 e = *reinterpret_cast<const f32x4*>(crow + u * 256 + lane * 4);
+    acc += (double)a[0] * e[0] + (double)a[1] * e[1] + (double)a[2] * e[2] + (double)a[3] * e[3];
+  }
+  return wave_sum_f64(acc);
+}
+
+__global__ void __launch_bounds__(256) vq_certify_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
                                                          const float* __restrict__ pv2, int ntiles, int tile_codes,
-                                                         const float* __restrict__ x,
-                                                         const float* __restrict__ x2, int dim,
-                                                         const float* __restrict__ code, float emax, float e2max,
-                                                         float cbound, int32_t* __restrict__ codes,
+                                                         long long rows, const float* __restrict__ x,
+                                                         const float* __restrict__ x2, const double* __restrict__ x2d,
+                                                         const float* __restrict__ xr2, int dim,
+                                                         const float* __restrict__ code,
+                                                         const double* __restrict__ e2d, double cx, float emax,
+                                                         float e2max, int32_t* __restrict__ codes,
+                                                         int2* __restrict__ pairs, long long cap,
+                                                         unsigned long long* __restrict__ npairs, int2* __restrict__ row_list,
                                                          int* __restrict__ stats) {
-  const long long row = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  __shared__ float s_v[4];
-  __shared__ int s_i[4], s_n[4];
-  __shared__ double s_d[4];
-  __shared__ int s_c[4];
-  __shared__ unsigned char flag[kMaxVqTiles];
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
   const float* v1p = pv + row * ntiles;
   const float* v2p = pv2 + row * ntiles;
   const int* i1p = pi + row * ntiles;
 
   // 1. best approximate value.  The bound takes |x|^2 from row_sqnorm (fp64 sum rounded to fp32,
-  // within 2^-24 relative), raised by 2^-20 so it is never below the exact value; the x row itself
-  // (14 KiB at 3584 channels) is read only by rows that go on to the rescore (~10 %).
+  // within 2^-24 relative), raised by 2^-20 so it is never below the exact value.
   float bv = __builtin_inff();
   int bi = 0x7fffffff;
-  for (int t = tid; t < ntiles; t += 256) {
+  for (int t = lane; t < ntiles; t += 64) {
     const float v = v1p[t];
     const int i = i1p[t];
     if (v < bv || (v == bv && i < bi)) { bv = v; bi = i; }
   }
-  const double xxb = (double)x2[row] * (1.0 + 0x1p-20);
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     const float ov = __shfl_xor(bv, off, 64);
     const int oi = __shfl_xor(bi, off, 64);
     if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
   }
-  if (lane == 0) { s_v[wave] = bv; s_i[wave] = bi; }
-  __syncthreads();
-  bv = s_v[0];
-  bi = s_i[0];
-#pragma unroll
-  for (int w = 1; w < 4; ++w)
-    if (s_v[w] < bv || (s_v[w] == bv && s_i[w] < bi)) { bv = s_v[w]; bi = s_i[w]; }
-
-  // 2. candidates inside the bound
-  const double bound = 2.0 * (double)cbound * sqrt(xxb) * (double)emax + 8.0 * 0x1p-24 * (xxb + (double)e2max);
+  const double xxb = (double)x2[row] * (1.0 + 0x1p-20);
+  // half-width of the prefilter's error: cx |x| (+ max|e| |x_r| for vq_prefilter_b1, whose x_r = x - bf16(x)
+  // comes from row_sqnorm, raised like |x|^2), plus the fp32 rounding of (|x|^2 + |e|^2) - 2 x.e
+  const double xrb = xr2 ? (double)xr2[row] * (1.0 + 0x1p-20) : 0.0;
+  const double bound = 2.0 * (cx * sqrt(xxb) + (double)emax * sqrt(xrb)) + 8.0 * 0x1p-24 * (xxb + (double)e2max);
   const double thr = (double)bv + 2.0 * bound * (1.0 + 1e-6);
+
+  // 2. candidates inside the bound; each lane counts those of its tiles (t = lane + 64 k)
   int cnt = 0;
-  for (int t = tid; t < ntiles; t += 256) {
+  for (int t = lane; t < ntiles; t += 64) {
     const double v1 = v1p[t], v2 = v2p[t];
-    const int f = v1 <= thr ? (v2 <= thr ? 2 : 1) : 0;
-    flag[t] = (unsigned char)f;
-    cnt += f == 2 ? tile_codes : f;
+    cnt += v1 <= thr ? (v2 <= thr ? tile_codes : 1) : 0;
   }
+  int pre = cnt;  // inclusive prefix over lanes
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
-  if (lane == 0) s_n[wave] = cnt;
-  __syncthreads();
-  cnt = s_n[0] + s_n[1] + s_n[2] + s_n[3];
-  if (cnt <= 1) {  // certified (cnt == 0 only for non-finite input: keep the prefilter's pick)
-    if (tid == 0) codes[row] = bi;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(pre, off, 64);
+    if (lane >= off) pre += o;
+  }
+  const int total = __shfl(pre, 63, 64);
+  if (total <= 1) {  // certified (0 only for non-finite input: keep the prefilter's pick)
+    if (lane == 0) {
+      codes[row] = bi;
+      row_list[row] = make_int2(-1, 0);
+    }
     return;
   }
-  if (stats && tid == 0) {
+  if (stats && lane == 0) {
     atomicAdd(&stats[0], 1);
-    atomicAdd(&stats[1], cnt);
+    atomicAdd(&stats[1], total);
   }
-
-  // 3. exact rescore of the candidates, one code per wave at a time; x and |x|^2 in fp64 (every
-  // wave holds the whole row)
-  const int nvec = dim >> 8;  // float4 per lane
-  f32x4 xr[kMaxVqDimVec];
-  double xx = 0;
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(npairs, (unsigned long long)total);
+  base = __shfl(base, 0, 64);
+  if (base + total <= (unsigned long long)cap) {
+    // 3a. list the candidates for vq_pair_eval_kernel
+    long long o = (long long)base + pre - cnt;
+    for (int t = lane; t < ntiles; t += 64) {
+      const double v1 = v1p[t], v2 = v2p[t];
+      if (!(v1 <= thr)) continue;  // the counting predicate exactly (NaN partials count nothing)
+      if (v2 <= thr)
+        for (int j = 0; j < tile_codes; ++j) pairs[o++] = make_int2((int)row, t * tile_codes + j);
+      else
+        pairs[o++] = make_int2((int)row, i1p[t]);
+    }
+    if (lane == 0) row_list[row] = make_int2((int)base, total);
+    return;
+  }
+  // 3b. list full: rescore here, one candidate at a time.  The part of the reserved block that lies
+  // inside the list gets sentinels, so vq_pair_eval_kernel never reads an entry this call did not write.
+  for (unsigned long long o = base + lane; o < (unsigned long long)cap; o += 64) pairs[o] = make_int2(-1, -1);
+  if (lane == 0) row_list[row] = make_int2(-1, 0);
+  const int nvec = dim >> 8;
   const float* xrow = x + row * dim;
-#pragma unroll
-  for (int u = 0; u < kMaxVqDimVec; ++u) {
-    xr[u] = u < nvec ? *reinterpret_cast<const f32x4*>(xrow + u * 256 + lane * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-    xx += (double)xr[u][0] * xr[u][0] + (double)xr[u][1] * xr[u][1] + (double)xr[u][2] * xr[u][2] +
-          (double)xr[u][3] * xr[u][3];
-  }
-  xx = wave_sum_f64(xx);
   double best = __builtin_inf();
   int bc = 0x7fffffff;
   auto eval = [&](int c) {
-    const float* crow = code + (long long)c * dim;
-    double dot = 0, ee = 0;
-#pragma unroll
-    for (int u = 0; u < kMaxVqDimVec; ++u) {
-      if (u < nvec) {
-        const f32x4 e = *reinterpret_cast<const f32x4*>(crow + u * 256 + lane * 4);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          dot += (double)xr[u][k] * e[k];
-          ee += (double)e[k] * e[k];
-        }
-      }
-    }
-    dot = wave_sum_f64(dot);
-    ee = wave_sum_f64(ee);
-    const double d = (xx + ee) - 2.0 * dot;
-    if (d < best || (d == best && c < bc)) { best = d; bc = c; }
+    const double d = (x2d[row] + e2d[c]) - 2.0 * dot_f64(xrow, code + (long long)c * dim, nvec, lane);
+    if (dless(d, c, best, bc)) { best = d; bc = c; }
   };
   for (int t = 0; t < ntiles; ++t) {
-    const int f = flag[t];
-    if (f == 1) {
-      if (wave == (t & 3)) eval(i1p[t]);
-    } else if (f == 2) {
-      for (int c = t * tile_codes + wave; c < (t + 1) * tile_codes; c += 4) eval(c);
-    }
+    const double v1 = v1p[t], v2 = v2p[t];
+    if (!(v1 <= thr)) continue;
+    if (v2 <= thr)
+      for (int c = t * tile_codes; c < (t + 1) * tile_codes; ++c) eval(c);
+    else
+      eval(i1p[t]);
   }
-  if (lane == 0) { s_d[wave] = best; s_c[wave] = bc; }
-  __syncthreads();
-  if (tid == 0) {
-    double d = s_d[0];
-    int c = s_c[0];
-    for (int w = 1; w < 4; ++w)
-      if (s_d[w] < d || (s_d[w] == d && s_c[w] < c)) { d = s_d[w]; c = s_c[w]; }
-    codes[row] = c;
+  if (lane == 0) codes[row] = bc;
+}
+
+__global__ void __launch_bounds__(256) vq_pair_eval_kernel(const int2* __restrict__ pairs,
+                                                           const unsigned long long* __restrict__ npairs,
+                                                           long long cap, long long rows, int ncodes,
+                                                           const float* __restrict__ x,
+                                                           const double* __restrict__ x2d, int dim,
+                                                           const float* __restrict__ code,
+                                                           const double* __restrict__ e2d, double* __restrict__ dist) {
+  const int lane = threadIdx.x & 63;
+  const long long n = (long long)min(*npairs, (unsigned long long)cap);
+  const long long nw = (long long)gridDim.x * 4;
+  const int nvec = dim >> 8;
+  for (long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); p < n; p += nw) {
+    const int2 rc = pairs[p];
+    if (rc.x < 0 || rc.x >= rows || rc.y < 0 || rc.y >= ncodes) continue;  // a sentinel (overflowed block)
+    const double dot = dot_f64(x + (long long)rc.x * dim, code + (long long)rc.y * dim, nvec, lane);
+    if (lane == 0) dist[p] = (x2d[rc.x] + e2d[rc.y]) - 2.0 * dot;
   }
 }
 
-hipError_t launch_vq_rescore(const float* part_val, const int* part_idx, const float* part_val2, long long rows,
-                             int ntiles, int tile_codes, const float* x, const float* x2, int dim,
-                             const float* codebook, float emax, float e2max, float cbound, int32_t* codes, int* stats,
-                             hipStream_t s) {
-  if (ntiles < 1 || ntiles > kMaxVqTiles || dim % 256 || dim > 256 * kMaxVqDimVec || rows < 0)
+__global__ void __launch_bounds__(256) vq_pair_reduce_kernel(const int2* __restrict__ row_list,
+                                                             const int2* __restrict__ pairs,
+                                                             const double* __restrict__ dist, long long rows,
+                                                             int32_t* __restrict__ codes) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int2 rl = row_list[row];
+  if (rl.x < 0) return;
+  double best = __builtin_inf();
+  int bc = 0x7fffffff;
+  for (int j = lane; j < rl.y; j += 64) {
+    const double d = dist[(long long)rl.x + j];
+    const int c = pairs[(long long)rl.x + j].y;
+    if (dless(d, c, best, bc)) { best = d; bc = c; }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double od = __shfl_xor(best, off, 64);
+    const int oc = __shfl_xor(bc, off, 64);
+    if (dless(od, oc, best, bc)) { best = od; bc = oc; }
+  }
+  if (lane == 0) codes[row] = bc;
+}
+
+hipError_t launch_vq_rescore(const VqRescoreArgs& a, hipStream_t s) {
+  if (a.ntiles < 1 || a.ntiles > kMaxVqTiles || a.dim % 256 || a.dim > 256 * kMaxVqDimVec || a.rows < 0 ||
+      a.rows > (1ll << 31) - 1 || !a.pairs || !a.dist || !a.row_list || !a.npairs || !a.x2d || !a.e2d)
     return hipErrorInvalidValue;
-  if (rows == 0) return hipSuccess;
-  hipLaunchKernelGGL(vq_rescore_kernel, dim3((unsigned)rows), dim3(256), 0, s, part_val, part_idx, part_val2, ntiles,
-                     tile_codes, x, x2, dim, codebook, emax, e2max, cbound, codes, stats);
+  if (a.rows == 0) return hipSuccess;
+  const unsigned blocks = (unsigned)((a.rows + 3) / 4);
+  hipLaunchKernelGGL(vq_certify_kernel, dim3(blocks), dim3(256), 0, s, a.part_val, a.part_idx, a.part_val2, a.ntiles,
+                     a.tile_codes, a.rows, a.x, a.x2, a.x2d, a.xr2, a.dim, a.codebook, a.e2d, a.cx, a.emax, a.e2max,
+                     a.codes, a.pairs, a.cap, a.npairs, a.row_list, a.stats);
+  // the pair count is known on the device only: enough waves to cover the list, at most 8 blocks per CU
+  const long long eb = std::min<long long>((a.cap + 3) / 4, 2048);
+  hipLaunchKernelGGL(vq_pair_eval_kernel, dim3((unsigned)std::max<long long>(eb, 1)), dim3(256), 0, s, a.pairs,
+                     a.npairs, a.cap, a.rows, a.ntiles * a.tile_codes, a.x, a.x2d, a.dim, a.codebook, a.e2d,
+                     a.dist);
+  hipLaunchKernelGGL(vq_pair_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.row_list, a.pairs, a.dist, a.rows,
+                     a.codes);
   return hipGetLastError();
 }
 

@@ -120,7 +120,7 @@ def test_codec_flag_switches_and_restores(codec, golden):
 
 @pytest.mark.parametrize("B,secs", [(2, 3), (4, 11)])
 def test_compact_layout_same_bits(beng, cfg, state, B, secs):
-    """bf16 mode stores the activations read by conv_gemm_bf16dm and vq_prefilter_bq in the compact
+    """bf16 mode stores the activations read by conv_gemm_bf16dm and vq_prefilter_b1 in the compact
     layout (hi plane only, 2 B per element).  The GEMMs read the same hi values either way, so the
     encoder features and x_pjt_in equal the planes-layout run (DCX_NO_COMPACT=1) bit for bit, and the
     codes too (both exact argmins).  4 x 11 s puts every 1x1 conv on conv_gemm_bf16dm; 2 x 3 s mixes

@@ -1,6 +1,7 @@
 """GPU VQ search in x6 mode against an exact fp64 argmin.
 
-x6 mode searches with a bf16x3 prefilter and then an fp64 rescore (launch_vq_prefilter /
+x6 mode searches with a one-product bf16 prefilter (vq_prefilter_b1; vq_prefilter_x3 on planes
+where it does not take the shape) and then an fp64 rescore (launch_vq_prefilter /
 vq_rescore_kernel). The prefilter's winner is accepted only when no other code can be inside
 its rigorous error bound. Every other row is rescored in fp64. The search must therefore return
 the exact nearest code for every row, with the lowest index on exact ties (the reference's
@@ -113,10 +114,10 @@ def test_workspace_without_generator(veng):
     assert 0 < ws < gen // 3
 
 
-def test_hm_layout_same_codes(veng, cfg, state):
-    """x6 mode hands x_pjt_in to vq_prefilter_dm in the "hm" layout (hi and mid planes per 32
-    channels) with the codebook repacked the same way; DCX_NO_COMPACT=1 keeps the planes layout.
-    Both searches are exact, so x_pjt_in and the codes agree bit for bit."""
+def test_compact_layout_same_codes(veng, cfg, state):
+    """x6 mode hands x_pjt_in to vq_prefilter_b1 in the compact bf16 layout with the codebook's hi
+    plane packed per K32 step; DCX_NO_COMPACT=1 keeps the planes layout (vq_prefilter_x3). Both
+    searches are exact, so x_pjt_in and the codes agree bit for bit."""
     import os
 
     from distilcodec_nabeel_amd.engine import NativeCodec
@@ -146,3 +147,61 @@ def test_search_exact_single_row_panel(veng, state, rows):
     feat = torch.randn(1, rows, 1024, generator=g) * 0.5
     codes, pin = _search(veng, feat)
     assert np.array_equal(codes, _argmin_fp64(pin, R.codebook(state["quantizer"])))
+
+
+def test_search_near_duplicates_exact(cfg, state):
+    """Codes that differ from each row's chosen code only below bf16 resolution (relative 1e-6
+    perturbations, in the same 256-code tile and in other tiles): the one-product prefilter sees
+    equal or nearly equal distances, so only the rescore can separate them. The search must
+    still return the exact fp64 argmin."""
+    from distilcodec_nabeel_amd.engine import NativeCodec
+    from oracle import reference_cpu as R
+
+    g = torch.Generator().manual_seed(13)
+    feat = torch.randn(2, 300, 1024, generator=g) * 0.5
+    base = NativeCodec(cfg, state, "cuda:0", with_generator=False, gemm="x6")
+    codes0, _ = _search(base, feat)
+    del base
+    E = R.codebook(state["quantizer"]).clone()
+    NC = E.shape[0]
+    chosen = sorted(set(codes0.tolist()))[:24]
+    for k, c in enumerate(chosen):
+        for t in (c ^ 3, (c + 256 * (k % 7 + 1)) % NC, (c + 9000) % NC):
+            if t in chosen:
+                continue
+            E[t] = E[c] * (1 + 1e-6 * torch.randn(E.shape[1], generator=g))
+    st = {k: dict(v) for k, v in state.items()}
+    st["quantizer"][KEY] = E[None].numpy() if isinstance(state["quantizer"][KEY], np.ndarray) else E[None]
+    eng = NativeCodec(cfg, st, "cuda:0", with_generator=False, gemm="x6")
+    eng.vq_rescore_stats(reset=True)
+    codes, pin = _search(eng, feat)
+    assert np.array_equal(codes, _argmin_fp64(pin, E))
+    rows, n = eng.vq_rescore_stats()
+    assert rows > 0 and n >= 2 * rows
+
+
+@pytest.mark.parametrize("per_row", ["0", "2"])
+def test_rescore_in_place_path_same_codes(veng, cfg, state, per_row):
+    """DCX_VQ_PAIRS_PER_ROW=0 leaves the rescore's candidate list no room, so every uncertified
+    row is rescored by its own wave in vq_certify_kernel (the overflow path) instead of through
+    vq_pair_eval_kernel / vq_pair_reduce_kernel; with 2 per row the list fills part way (rows
+    listed, then an overflowing block padded with sentinels, then rows rescored in place). The
+    same fp64 arithmetic either way, so the same codes."""
+    import os
+
+    from distilcodec_nabeel_amd.engine import NativeCodec
+
+    os.environ["DCX_VQ_PAIRS_PER_ROW"] = per_row
+    try:
+        inplace = NativeCodec(cfg, {"encoder": state["encoder"], "quantizer": state["quantizer"]}, "cuda:0",
+                              with_generator=False, gemm="x6")
+    finally:
+        del os.environ["DCX_VQ_PAIRS_PER_ROW"]
+    g = torch.Generator().manual_seed(21)
+    feat = (torch.randn(2, 400, 1024, generator=g) * 0.6).cuda()
+    a = veng.vq_encode(feat, want_fup=False, want_quantized=False)
+    inplace.vq_rescore_stats(reset=True)
+    b = inplace.vq_encode(feat, want_fup=False, want_quantized=False)
+    rows, _ = inplace.vq_rescore_stats()
+    assert rows > 0
+    assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])

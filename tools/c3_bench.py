@@ -61,7 +61,7 @@ def main():
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / a.steps
         # per-kernel HIP-event timing of one more step: the dominant kernel against its MFMA ceiling
-        # (products per fp32-equivalent FLOP: 1 for bf16 GEMMs, 2 for the bf16-mode prefilter, 6 / 3 in x6)
+        # (products per fp32-equivalent FLOP: 1 for bf16 GEMMs and vq_prefilter_b1, 2 for vq_prefilter_bq, 6 / 3 in x6)
         eng.profile(True)
         eng.profile_reset()
         step()
@@ -70,7 +70,7 @@ def main():
         if a.kernels:
             json.dump({"steps": 1, "kernels": kern}, open(f"{a.kernels}_{mode}.json", "w"), indent=1)
         name, rec = max(kern.items(), key=lambda kv: kv[1]["ms"])
-        prods = 2 if "prefilter_bk" in name or "prefilter_bq" in name or "_x2" in name else 3 if "prefilter" in name else 1 if "bf16" in name else 6
+        prods = 1 if "prefilter_b1" in name else 2 if "prefilter_bk" in name or "prefilter_bq" in name or "_x2" in name else 3 if "prefilter" in name else 1 if "bf16" in name else 6
         ach = rec["flops"] / (rec["ms"] * 1e-3) / 1e12
         roof = {"bound": "mfma", "kernel": name, "achieved": round(ach, 1), "peak": round(2500.0 / prods, 1),
                 "unit": "TFLOP/s (fp32-equivalent)", "frac": round(ach * prods / 2500.0, 4),
