@@ -108,6 +108,7 @@ struct dcx_codec {
   float emax = 0.f, e2max = 0.f;  // largest codebook row norm / squared norm (prefilter bound)
   float dmax = 0.f;               // largest |e - bf16(e)| over the codes (vq_prefilter_b1's bound)
   int* vq_stats = nullptr;        // [rows rescored, codes rescored] (dcx_vq_rescore_stats)
+  bool vq_stats_on = false;       // counted from the first dcx_vq_rescore_stats call on
   unsigned short* codebook6 = nullptr;
   unsigned short* codebook_bk = nullptr;  // hi/mid per K32 step (vq_prefilter_bq / _dm; DCX_VQ_OLD builds)
   unsigned short* codebook_b1 = nullptr;  // [CD/32][NC][32] bf16 hi (vq_prefilter_b1)
@@ -870,7 +871,8 @@ int vq_xlayout(const dcx_codec* h, long long M) {
 struct VqScratch {
   float *x2 = nullptr, *xr2 = nullptr, *pv = nullptr, *pv2 = nullptr;
   int* pi = nullptr;
-  double *x2d = nullptr, *dist = nullptr;
+  double *x2d = nullptr, *cdist = nullptr;
+  int* ccode = nullptr;
   int2 *pairs = nullptr, *row_list = nullptr;
   unsigned long long* npairs = nullptr;
   long long cap = 0;
@@ -884,9 +886,10 @@ VqScratch vq_scratch(const dcx_codec* h, Bump& ws, long long M, int ntiles, bool
     v.xr2 = ws.f((size_t)M);
     v.pv2 = ws.f((size_t)M * ntiles);
     v.x2d = (double*)ws.raw((size_t)M * sizeof(double));
-    v.cap = h->vq_pairs_per_row > 0 ? std::max<long long>((long long)h->vq_pairs_per_row * M, 1024) : 0;
+    v.cap = h->vq_pairs_per_row > 0 ? std::max<long long>((long long)h->vq_pairs_per_row * M, 1024) / 8 * 8 : 0;
     v.pairs = (int2*)ws.raw((size_t)v.cap * sizeof(int2));
-    v.dist = (double*)ws.raw((size_t)v.cap * sizeof(double));
+    v.cdist = (double*)ws.raw((size_t)(v.cap / 8) * sizeof(double));
+    v.ccode = ws.i((size_t)(v.cap / 8));
     v.row_list = (int2*)ws.raw((size_t)M * sizeof(int2));
     v.npairs = (unsigned long long*)ws.raw(sizeof(unsigned long long));
   }
@@ -928,9 +931,11 @@ int run_vq_search(dcx_codec* h, const float* P, const unsigned short* P6, int xl
     a.x = P; a.x2 = x2; a.xr2 = b1 ? v.xr2 : nullptr; a.x2d = v.x2d;
     a.codebook = h->codebook; a.e2d = h->e2d;
     a.cx = dcx::vq_prefilter_cx(xl, NC, CD, h->emax, h->dmax); a.emax = h->emax; a.e2max = h->e2max;
-    a.codes = codes; a.stats = h->vq_stats;
-    a.pairs = v.pairs; a.dist = v.dist; a.cap = v.cap; a.row_list = v.row_list; a.npairs = v.npairs;
-    LAUNCH(h, s, "vq_rescore", 0, 12.0 * M * ntiles + 4.0 * M, dcx::launch_vq_rescore(a, s));
+    a.codes = codes; a.stats = h->vq_stats_on ? h->vq_stats : nullptr;
+    a.pairs = v.pairs; a.cdist = v.cdist; a.ccode = v.ccode; a.cap = v.cap; a.row_list = v.row_list; a.npairs = v.npairs;
+    LAUNCH(h, s, "vq_certify", 0, 12.0 * M * ntiles + 4.0 * M, dcx::launch_vq_certify(a, s));
+    LAUNCH(h, s, "vq_pair_eval", 0, 0, dcx::launch_vq_pair_eval(a, s));
+    LAUNCH(h, s, "vq_pair_reduce", 0, 0, dcx::launch_vq_pair_reduce(a, s));
   } else {
     LAUNCH(h, s, "vq_reduce", 0, 8.0 * M * ntiles, dcx::launch_vq_reduce(v.pv, v.pi, (int)M, ntiles, codes, s));
   }
@@ -1884,6 +1889,7 @@ int dcx_profile_reset(dcx_codec* h) {
 
 int dcx_vq_rescore_stats(dcx_codec* h, int64_t* rows_rescored, int64_t* codes_rescored, int32_t reset) {
   if (!h || !h->vq_stats) return DCX_ERR_STATE;
+  h->vq_stats_on = true;
   int v[2] = {0, 0};
   if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(v, h->vq_stats, sizeof v, hipMemcpyDeviceToHost) != hipSuccess)
     return fail(h, DCX_ERR_HIP, "reading VQ rescore counters failed");

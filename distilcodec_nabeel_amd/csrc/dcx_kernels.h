@@ -137,8 +137,8 @@ double vq_prefilter_cx(int x_layout, int ncodes, int dim, float emax, float dmax
 // vq_rescore arguments.  part_*: the prefilter's [rows][ntiles] partials; x: x_pjt_in fp32
 // [rows][dim]; x2 / x2d: |x|^2 per row (row_sqnorm, fp32 / fp64); xr2 (optional): |x - bf16(x)|^2,
 // required for vq_prefilter_b1's bound; e2d: |e|^2 per code in fp64; cx / emax / e2max: the bound
-// (vq_prefilter_cx).  Workspace: pairs / dist [cap] candidate list, row_list [rows], npairs (zeroed
-// by row_sqnorm before the prefilter).  stats (optional): [0] rows rescored, [1] codes rescored.
+// (vq_prefilter_cx).  Workspace: pairs [cap] candidate list (cap a multiple of 8), cdist / ccode
+// [cap / 8] per-chunk results, row_list [rows], npairs (zeroed by row_sqnorm before the prefilter).  stats (optional): [0] rows rescored, [1] codes rescored.
 struct VqRescoreArgs {
   const float *part_val, *part_val2;
   const int* part_idx;
@@ -153,12 +153,16 @@ struct VqRescoreArgs {
   int32_t* codes;
   int* stats;
   int2* pairs;
-  double* dist;
+  double* cdist;
+  int* ccode;
   long long cap;
   int2* row_list;
   unsigned long long* npairs;
 };
-hipError_t launch_vq_rescore(const VqRescoreArgs& a, hipStream_t s);
+// the rescore's three launches, in this order (vq_certify lists, vq_pair_eval evaluates, vq_pair_reduce picks)
+hipError_t launch_vq_certify(const VqRescoreArgs& a, hipStream_t s);
+hipError_t launch_vq_pair_eval(const VqRescoreArgs& a, hipStream_t s);
+hipError_t launch_vq_pair_reduce(const VqRescoreArgs& a, hipStream_t s);
 hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows, int ntiles, int32_t* codes,
                             hipStream_t s);
 // x2 (fp32) and optionally x2d (fp64) |x|^2, xr2 |x - bf16(x)|^2 per row; zero_me (optional) set to 0

@@ -377,14 +377,18 @@ hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows
 // latency-bound (one workgroup per row: 9.9 ms at C3, 4.3 ms at C2):
 //   vq_certify_kernel    one wave per row: certifies, or reserves a contiguous block of
 //                        (row, code) pairs in the workspace list (a vector atomicAdd on one
-//                        counter) and writes the row's candidates there in tile order;
-//   vq_pair_eval_kernel  one wave per pair: d = (|x|^2 + |e|^2) - 2 x.e in fp64 (|x|^2 and |e|^2
-//                        the fp64 sums of row_sqnorm and of the load-time codebook pass);
-//   vq_pair_reduce_kernel one wave per listed row: smallest d, lowest code on exact ties.
+//                        counter), rounded up to chunks of kVqChunk with sentinel padding, and
+//                        writes the row's candidates there in tile order;
+//   vq_pair_eval_kernel  one wave per chunk: x once into registers, then for each listed code
+//                        d = (|x|^2 + |e|^2) - 2 x.e in fp64 (|x|^2 and |e|^2 the fp64 sums of
+//                        row_sqnorm and of the load-time codebook pass); the chunk's best (d, code);
+//   vq_pair_reduce_kernel one wave per listed row: smallest d over its chunks, lowest code on ties.
+// (One wave per pair, x re-read for every candidate, moved 1.6x the bytes: 8.2 ms at C3.)
 // A row whose candidates would overflow the list is rescored by its own wave in the certify
 // kernel (the same fp64 arithmetic), so the result never depends on the list capacity.
 constexpr int kMaxVqTiles = 512;
 constexpr int kMaxVqDimVec = 16;  // dim <= 16 * 256
+constexpr int kVqChunk = 8;       // candidate pairs per vq_pair_eval_kernel work item
 
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll
@@ -393,20 +397,54 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 }
 __device__ __forceinline__ bool dless(double d, int c, double bd, int bc) { return d < bd || (d == bd && c < bc); }
 
-// x.e in fp64 over one wave (lane-strided float4s; every lane returns the sum)
-__device__ __forceinline__ double dot_f64(const float* __restrict__ xrow, const float* __restrict__ crow, int nvec,
-                                          int lane) {
+// One row of dim = 256 nvec floats as lane-strided float4s.  Every load is issued unconditionally
+// (index clamped; the extra ones re-read the last float4 and are dropped by the caller), so all of
+// them are in flight at once: loads under `if (u < nvec)` went out one round trip at a time.
+__device__ __forceinline__ void load_row(f32x4 (&v)[kMaxVqDimVec], const float* __restrict__ row, int nvec, int lane) {
+#pragma unroll
+  for (int u = 0; u < kMaxVqDimVec; ++u)
+    v[u] = *reinterpret_cast<const f32x4*>(row + min(u, nvec - 1) * 256 + lane * 4);
+}
+// x.e in fp64 over one wave, both rows streamed in quarters (the in-place path of vq_certify_kernel,
+// whose 1024-thread workgroups leave 128 VGPRs per lane)
+__device__ __forceinline__ double dot_stream_f64(const float* __restrict__ xrow, const float* __restrict__ crow,
+                                                 int nvec, int lane) {
+  constexpr int H = kMaxVqDimVec / 4;
   double acc = 0;
-#pragma unroll 7
-  for (int u = 0; u < nvec; ++u) {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(xrow + u * 256 + lane * 4);
-    const f32x4 e = *reinterpret_cast<const f32x4*>(crow + u * 256 + lane * 4);
-    acc += (double)a[0] * e[0] + (double)a[1] * e[1] + (double)a[2] * e[2] + (double)a[3] * e[3];
+#pragma nounroll
+  for (int h = 0; h < 4; ++h) {
+    f32x4 a[H], e[H];
+#pragma unroll
+    for (int u = 0; u < H; ++u) {
+      const int uu = min(h * H + u, nvec - 1);
+      a[u] = *reinterpret_cast<const f32x4*>(xrow + uu * 256 + lane * 4);
+      e[u] = *reinterpret_cast<const f32x4*>(crow + uu * 256 + lane * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < H; ++u)
+      if (h * H + u < nvec)
+        acc += (double)a[u][0] * e[u][0] + (double)a[u][1] * e[u][1] + (double)a[u][2] * e[u][2] +
+               (double)a[u][3] * e[u][3];
   }
   return wave_sum_f64(acc);
 }
+// x.e in fp64 over one wave, x held in registers (every lane returns the sum)
+__device__ __forceinline__ double dot_f64(const f32x4 (&xr)[kMaxVqDimVec], const float* __restrict__ crow, int nvec,
+                                          int lane) {
+  f32x4 e[kMaxVqDimVec];
+  load_row(e, crow, nvec, lane);
+  double acc = 0;
+#pragma unroll
+  for (int u = 0; u < kMaxVqDimVec; ++u)
+    if (u < nvec)
+      acc += (double)xr[u][0] * e[u][0] + (double)xr[u][1] * e[u][1] + (double)xr[u][2] * e[u][2] +
+             (double)xr[u][3] * e[u][3];
+  return wave_sum_f64(acc);
+}
 
-__global__ void __launch_bounds__(256) vq_certify_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
+constexpr int kCertifyRows = 16;  // rows (waves) per vq_certify_kernel workgroup: one list atomic per workgroup
+
+__global__ void __launch_bounds__(64 * kCertifyRows) vq_certify_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
                                                          const float* __restrict__ pv2, int ntiles, int tile_codes,
                                                          long long rows, const float* __restrict__ x,
                                                          const float* __restrict__ x2, const double* __restrict__ x2d,
@@ -417,9 +455,12 @@ __global__ void __launch_bounds__(256) vq_certify_kernel(const float* __restrict
                                                          int2* __restrict__ pairs, long long cap,
                                                          unsigned long long* __restrict__ npairs, int2* __restrict__ row_list,
                                                          int* __restrict__ stats) {
-  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __shared__ int s_n[kCertifyRows];
+  __shared__ unsigned long long s_base;
+  // rows past the end take part in the workgroup's list reservation with nothing to list
+  const bool live = (long long)blockIdx.x * kCertifyRows + wave < rows;
+  const long long row = live ? (long long)blockIdx.x * kCertifyRows + wave : rows - 1;
   const float* v1p = pv + row * ntiles;
   const float* v2p = pv2 + row * ntiles;
   const int* i1p = pi + row * ntiles;
@@ -446,19 +487,39 @@ __global__ void __launch_bounds__(256) vq_certify_kernel(const float* __restrict
   const double bound = 2.0 * (cx * sqrt(xxb) + (double)emax * sqrt(xrb)) + 8.0 * 0x1p-24 * (xxb + (double)e2max);
   const double thr = (double)bv + 2.0 * bound * (1.0 + 1e-6);
 
-  // 2. candidates inside the bound; each lane counts those of its tiles (t = lane + 64 k)
-  int cnt = 0;
+  // 2. candidates inside the bound; each lane counts those of its tiles (t = lane + 64 k): single codes
+  // (the tile's smallest only) and whole tiles (its second smallest inside the bound too)
+  int cnt = 0, nwhole = 0;
   for (int t = lane; t < ntiles; t += 64) {
     const double v1 = v1p[t], v2 = v2p[t];
-    cnt += v1 <= thr ? (v2 <= thr ? tile_codes : 1) : 0;
+    if (v1 <= thr) {
+      if (v2 <= thr) ++nwhole;
+      else ++cnt;
+    }
   }
-  int pre = cnt;  // inclusive prefix over lanes
+  int pre = cnt;  // inclusive prefix of the single codes over lanes
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const int o = __shfl_up(pre, off, 64);
     if (lane >= off) pre += o;
   }
-  const int total = __shfl(pre, 63, 64);
+  int wsum = nwhole;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) wsum += __shfl_xor(wsum, off, 64);
+  const int nsingle = __shfl(pre, 63, 64);
+  const int total = live ? nsingle + wsum * tile_codes : 0;
+  // whole chunks (cap is a multiple too); one atomicAdd per workgroup reserves every row's block
+  // (an atomic per row on the one counter serialised 150k times at C3)
+  const int rtot = total <= 1 ? 0 : (total + kVqChunk - 1) / kVqChunk * kVqChunk;
+  if (lane == 0) s_n[wave] = rtot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int sum = 0;
+    for (int w = 0; w < kCertifyRows; ++w) sum += s_n[w];
+    s_base = sum ? atomicAdd(npairs, (unsigned long long)sum) : 0;
+  }
+  __syncthreads();
+  if (!live) return;
   if (total <= 1) {  // certified (0 only for non-finite input: keep the prefilter's pick)
     if (lane == 0) {
       codes[row] = bi;
@@ -470,20 +531,30 @@ __global__ void __launch_bounds__(256) vq_certify_kernel(const float* __restrict
     atomicAdd(&stats[0], 1);
     atomicAdd(&stats[1], total);
   }
-  unsigned long long base = 0;
-  if (lane == 0) base = atomicAdd(npairs, (unsigned long long)total);
-  base = __shfl(base, 0, 64);
-  if (base + total <= (unsigned long long)cap) {
-    // 3a. list the candidates for vq_pair_eval_kernel
+  unsigned long long base = s_base;
+  for (int w = 0; w < wave; ++w) base += s_n[w];
+  if (base + rtot <= (unsigned long long)cap) {
+    // 3a. list the candidates for vq_pair_eval_kernel: the single codes (each lane its own), then
+    // the whole tiles, written by the whole wave (one lane writing 256 entries held its workgroup of
+    // 16 rows for ~100 us: 1.7 ms at C2)
     long long o = (long long)base + pre - cnt;
     for (int t = lane; t < ntiles; t += 64) {
       const double v1 = v1p[t], v2 = v2p[t];
-      if (!(v1 <= thr)) continue;  // the counting predicate exactly (NaN partials count nothing)
-      if (v2 <= thr)
-        for (int j = 0; j < tile_codes; ++j) pairs[o++] = make_int2((int)row, t * tile_codes + j);
-      else
-        pairs[o++] = make_int2((int)row, i1p[t]);
+      if (v1 <= thr && !(v2 <= thr)) pairs[o++] = make_int2((int)row, i1p[t]);  // the counting predicates
     }
+    long long ow = (long long)base + nsingle;
+    for (int tb = 0; tb < ntiles; tb += 64) {
+      const int t = tb + lane;
+      const bool whole = t < ntiles && (double)v1p[t] <= thr && (double)v2p[t] <= thr;
+      unsigned long long mask = __ballot(whole);
+      while (mask) {
+        const int k = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        for (int j = lane; j < tile_codes; j += 64) pairs[ow + j] = make_int2((int)row, (tb + k) * tile_codes + j);
+        ow += tile_codes;
+      }
+    }
+    if (lane < rtot - total) pairs[base + total + lane] = make_int2(-1, -1);
     if (lane == 0) row_list[row] = make_int2((int)base, total);
     return;
   }
@@ -496,7 +567,7 @@ __global__ void __launch_bounds__(256) vq_certify_kernel(const float* __restrict
   double best = __builtin_inf();
   int bc = 0x7fffffff;
   auto eval = [&](int c) {
-    const double d = (x2d[row] + e2d[c]) - 2.0 * dot_f64(xrow, code + (long long)c * dim, nvec, lane);
+    const double d = (x2d[row] + e2d[c]) - 2.0 * dot_stream_f64(xrow, code + (long long)c * dim, nvec, lane);
     if (dless(d, c, best, bc)) { best = d; bc = c; }
   };
   for (int t = 0; t < ntiles; ++t) {
@@ -516,33 +587,50 @@ __global__ void __launch_bounds__(256) vq_pair_eval_kernel(const int2* __restric
                                                            const float* __restrict__ x,
                                                            const double* __restrict__ x2d, int dim,
                                                            const float* __restrict__ code,
-                                                           const double* __restrict__ e2d, double* __restrict__ dist) {
+                                                           const double* __restrict__ e2d, double* __restrict__ cdist,
+                                                           int* __restrict__ ccode) {
   const int lane = threadIdx.x & 63;
-  const long long n = (long long)min(*npairs, (unsigned long long)cap);
+  const long long nch = (long long)min(*npairs, (unsigned long long)cap) / kVqChunk;
   const long long nw = (long long)gridDim.x * 4;
   const int nvec = dim >> 8;
-  for (long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); p < n; p += nw) {
-    const int2 rc = pairs[p];
-    if (rc.x < 0 || rc.x >= rows || rc.y < 0 || rc.y >= ncodes) continue;  // a sentinel (overflowed block)
-    const double dot = dot_f64(x + (long long)rc.x * dim, code + (long long)rc.y * dim, nvec, lane);
-    if (lane == 0) dist[p] = (x2d[rc.x] + e2d[rc.y]) - 2.0 * dot;
+  for (long long q = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); q < nch; q += nw) {
+    const int2 my = lane < kVqChunk ? pairs[q * kVqChunk + lane] : make_int2(-1, -1);
+    const int row = __shfl(my.x, 0, 64);
+    if (row < 0 || row >= rows) continue;  // a chunk of sentinels (overflowed block)
+    f32x4 xr[kMaxVqDimVec];
+    load_row(xr, x + (long long)row * dim, nvec, lane);
+    const double xx = x2d[row];
+    double best = __builtin_inf();
+    int bc = 0x7fffffff;
+    for (int k = 0; k < kVqChunk; ++k) {
+      const int r = __shfl(my.x, k, 64), c = __shfl(my.y, k, 64);
+      if (r != row || c < 0 || c >= ncodes) continue;  // padding
+      const double d = (xx + e2d[c]) - 2.0 * dot_f64(xr, code + (long long)c * dim, nvec, lane);
+      if (dless(d, c, best, bc)) { best = d; bc = c; }
+    }
+    if (lane == 0) {
+      cdist[q] = best;
+      ccode[q] = bc;
+    }
   }
 }
 
 __global__ void __launch_bounds__(256) vq_pair_reduce_kernel(const int2* __restrict__ row_list,
-                                                             const int2* __restrict__ pairs,
-                                                             const double* __restrict__ dist, long long rows,
+                                                             const double* __restrict__ cdist,
+                                                             const int* __restrict__ ccode, long long rows,
                                                              int32_t* __restrict__ codes) {
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int2 rl = row_list[row];
   if (rl.x < 0) return;
+  const long long q0 = rl.x / kVqChunk;
+  const int nq = (rl.y + kVqChunk - 1) / kVqChunk;
   double best = __builtin_inf();
   int bc = 0x7fffffff;
-  for (int j = lane; j < rl.y; j += 64) {
-    const double d = dist[(long long)rl.x + j];
-    const int c = pairs[(long long)rl.x + j].y;
+  for (int j = lane; j < nq; j += 64) {
+    const double d = cdist[q0 + j];
+    const int c = ccode[q0 + j];
     if (dless(d, c, best, bc)) { best = d; bc = c; }
   }
 #pragma unroll
@@ -554,22 +642,38 @@ __global__ void __launch_bounds__(256) vq_pair_reduce_kernel(const int2* __restr
   if (lane == 0) codes[row] = bc;
 }
 
-hipError_t launch_vq_rescore(const VqRescoreArgs& a, hipStream_t s) {
-  if (a.ntiles < 1 || a.ntiles > kMaxVqTiles || a.dim % 256 || a.dim > 256 * kMaxVqDimVec || a.rows < 0 ||
-      a.rows > (1ll << 31) - 1 || !a.pairs || !a.dist || !a.row_list || !a.npairs || !a.x2d || !a.e2d)
-    return hipErrorInvalidValue;
+static bool rescore_args_ok(const VqRescoreArgs& a) {
+  return a.ntiles >= 1 && a.ntiles <= kMaxVqTiles && a.dim % 256 == 0 && a.dim <= 256 * kMaxVqDimVec && a.rows >= 0 &&
+         a.rows <= (1ll << 31) - 1 && a.cap % kVqChunk == 0 && a.pairs && a.cdist && a.ccode && a.row_list &&
+         a.npairs && a.x2d && a.e2d;
+}
+
+hipError_t launch_vq_certify(const VqRescoreArgs& a, hipStream_t s) {
+  if (!rescore_args_ok(a)) return hipErrorInvalidValue;
   if (a.rows == 0) return hipSuccess;
-  const unsigned blocks = (unsigned)((a.rows + 3) / 4);
-  hipLaunchKernelGGL(vq_certify_kernel, dim3(blocks), dim3(256), 0, s, a.part_val, a.part_idx, a.part_val2, a.ntiles,
-                     a.tile_codes, a.rows, a.x, a.x2, a.x2d, a.xr2, a.dim, a.codebook, a.e2d, a.cx, a.emax, a.e2max,
-                     a.codes, a.pairs, a.cap, a.npairs, a.row_list, a.stats);
+  hipLaunchKernelGGL(vq_certify_kernel, dim3((unsigned)((a.rows + kCertifyRows - 1) / kCertifyRows)),
+                     dim3(64 * kCertifyRows), 0, s, a.part_val, a.part_idx, a.part_val2, a.ntiles, a.tile_codes,
+                     a.rows, a.x, a.x2, a.x2d, a.xr2, a.dim, a.codebook, a.e2d, a.cx, a.emax, a.e2max, a.codes, a.pairs,
+                     a.cap, a.npairs, a.row_list, a.stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_vq_pair_eval(const VqRescoreArgs& a, hipStream_t s) {
+  if (!rescore_args_ok(a)) return hipErrorInvalidValue;
+  if (a.rows == 0) return hipSuccess;
   // the pair count is known on the device only: enough waves to cover the list, at most 8 blocks per CU
-  const long long eb = std::min<long long>((a.cap + 3) / 4, 2048);
+  const long long eb = std::min<long long>((a.cap / kVqChunk + 3) / 4, 2048);
   hipLaunchKernelGGL(vq_pair_eval_kernel, dim3((unsigned)std::max<long long>(eb, 1)), dim3(256), 0, s, a.pairs,
                      a.npairs, a.cap, a.rows, a.ntiles * a.tile_codes, a.x, a.x2d, a.dim, a.codebook, a.e2d,
-                     a.dist);
-  hipLaunchKernelGGL(vq_pair_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.row_list, a.pairs, a.dist, a.rows,
-                     a.codes);
+                     a.cdist, a.ccode);
+  return hipGetLastError();
+}
+
+hipError_t launch_vq_pair_reduce(const VqRescoreArgs& a, hipStream_t s) {
+  if (!rescore_args_ok(a)) return hipErrorInvalidValue;
+  if (a.rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(vq_pair_reduce_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a.row_list, a.cdist,
+                     a.ccode, a.rows, a.codes);
   return hipGetLastError();
 }
 

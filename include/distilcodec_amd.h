@@ -227,10 +227,11 @@ size_t dcx_module_workspace_size(const dcx_codec* h, const char* module, int32_t
 int dcx_module_forward(dcx_codec* h, const char* module, const float* x, int32_t batch, int64_t rows, void* y,
                        void* workspace, size_t ws_bytes, void* stream);
 
-/* VQ search diagnostics (x6 mode): the search is a bf16x3 prefilter whose winner is certified
+/* VQ search diagnostics (x6 / bf16 mode): the search is a bf16 prefilter whose winner is certified
  * by a rigorous error bound; rows with more than one code inside the bound are rescored in fp64.
  * Returns the cumulative number of such rows and of codes rescored (synchronises the device);
- * reset != 0 zeroes the counters.  Replaces nothing in the reference (its search is one cdist). */
+ * reset != 0 zeroes the counters.  Counting is off until the first call (it costs two atomics per
+ * rescored row) and stays on from then.  Replaces nothing in the reference (its search is one cdist). */
 int dcx_vq_rescore_stats(dcx_codec* h, int64_t* rows_rescored, int64_t* codes_rescored, int32_t reset);
 
 /* Optional per-kernel timing: when enabled, every launch is bracketed by HIP events on its
