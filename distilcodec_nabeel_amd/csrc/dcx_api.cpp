@@ -122,7 +122,7 @@ struct dcx_codec {
   bool compact = true;
   // rescore candidate-list capacity per searched row (VqScratch); DCX_VQ_PAIRS_PER_ROW at dcx_create
   // (0: every uncertified row is rescored in place, the overflow path; tests)
-  int vq_pairs_per_row = 64;
+  int vq_pairs_per_row = 128;
   // split-K latency mode (dcx_set_split_k): at most split_k K-slices per few-tile x6 conv; the
   // partial sums live in the first kSplitScratch bytes of each stage call's workspace.  split_buf
   // points there only for the duration of one stage call (CallScope), which `busy` makes exclusive.
@@ -867,7 +867,7 @@ int vq_xlayout(const dcx_codec* h, long long M) {
 // 1 compact bf16, 2 hm): |x|^2, the certified prefilter and the fp64 rescore (x6 / bf16), or the exact
 // fp32 distance GEMM and its reduce (fp32 mode).  pv / pi / pv2: [M][ntiles] scratch, x2: [M].
 // Workspace of one search of M rows: the prefilter's [M][ntiles] partials and, in x6 / bf16 mode, the
-// rescore's candidate list (64 pairs per row on average; a row that does not fit is rescored in place).
+// rescore's candidate list (128 pairs per row on average: the C2 workload lists 62 in x6 mode; a row that does not fit is rescored in place).
 struct VqScratch {
   float *x2 = nullptr, *xr2 = nullptr, *pv = nullptr, *pv2 = nullptr;
   int* pi = nullptr;
