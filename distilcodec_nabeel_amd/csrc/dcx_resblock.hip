@@ -52,7 +52,9 @@ __device__ __forceinline__ void rp_wait(int n) {
   case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
   switch (n) {
     RP_W(1) RP_W(2) RP_W(3) RP_W(4) RP_W(5) RP_W(6) RP_W(7) RP_W(8) RP_W(9) RP_W(10) RP_W(11) RP_W(12)
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    RP_W(13) RP_W(14) RP_W(15) RP_W(16) RP_W(17) RP_W(18) RP_W(19) RP_W(20) RP_W(21) RP_W(22) RP_W(23) RP_W(24)
+    RP_W(25) RP_W(26) RP_W(27) RP_W(28) RP_W(29) RP_W(30) RP_W(31) RP_W(32)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // n > 32 waits for more: always safe
   }
 #undef RP_W
 }
@@ -110,6 +112,9 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
   // ---- weight ring: LDS-DMA of a step's taps (lane-linear 1 KiB pieces, no staging registers);
   // taps past the conv's last read zeros (outside the buffer descriptor) and are never used ----
   auto issue_w = [&](int m, int conv, int step, int slot) {
+#ifdef RP_DIAG_NODMA  // timing build: weights never refilled after the prologue (wrong results)
+    if (step > 0 || conv > 0 || m > 0) return;
+#endif
     const int k = p.taps[m], j0 = step * TPS;
     const unsigned short* w = (conv ? p.w2[m] : p.w1[m]) + (long long)j0 * (WTAP / 2);
     const __amdgpu_buffer_rsrc_t rw =
@@ -249,7 +254,9 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
         RP_T(s1);
         mfma_step(acc, slot, min(TPS, k - j * TPS), G::H1 + (j * TPS - hk) * d, d, RB, no_hook);
         RP_T(s2);
+#ifndef RP_DIAG_NOWAIT  // timing build: the next slot's pieces are not waited for (wrong results)
         rp_wait(0);
+#endif
         rp_barrier();
 #ifdef RP_DIAG_STAMPS
         {
@@ -339,7 +346,9 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
       for (int j = jpf + 1; j < nst; ++j) {
         c2_issue_w(j);
         mfma_step(acc, slot, min(TPS, k - j * TPS), 8 + j * TPS - hk, 1, nrb2, no_hook);
+#ifndef RP_DIAG_NOWAIT
         rp_wait(0);
+#endif
         rp_barrier();
         slot ^= 1;
       }
@@ -393,6 +402,273 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
 #endif
 }
 
+// Barrier-free tap loops (round 3): conv_res_pair_g.  conv_res_pair's per-step stamps put a c1 tap
+// step at 3690 cycles against 2304 of MFMA issue per SIMD (C = 64).  A timing build that never
+// refilled the weight ring was no faster, and a 4-slot ring of half-tap units with the next unit's
+// fragments prefetched into registers took 2278 cycles per 1152-cycle unit: every barrier of the
+// ring costs ~1100 cycles (the 8 waves restart together behind one LDS queue, and the slowest wave
+// sets the end), however short the step.  Here each wave loads its weight fragments from global
+// memory (L2; the four waves of a column half read the same bytes, so most hit L1) into registers,
+// chunk by chunk, one tap ahead: after the MFMAs of chunk ch of tap j, the registers take chunk ch
+// of the next tap in the stream (next conv, member or tile).  The tap loops need no barrier; only the
+// image hand-offs do (S -> T after c1, T -> the next S after c2).  Arithmetic, summation order and
+// layouts are conv_res_pair's, so the results are the same bits.
+template <int C, bool MEAN>
+__global__ void __launch_bounds__(512, 1) conv_res_pair_g(const ResPairParams p) {
+  using G = RpGeom<C>;
+  constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB1, BLK = G::BLK, IMG = G::IMG;
+  constexpr int G8 = G::G8, NIT = G::NIT, NS = G::NS, WTAP = G::WTAP;
+  __shared__ __attribute__((aligned(16))) char lds[IMG + 2 * kMaxGroup * C * 4];
+  float* const bias_lds = reinterpret_cast<float*>(lds + IMG);  // [conv][member][C]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wc = wave % G::WC, wr = wave / G::WC;
+  const int l15 = lane & 15, hf = (lane >> 4) & 1, t = lane >> 5;
+  const int L = p.L, nmem = p.nmem;
+  const int ntl = (L + R - 1) / R;
+  const int total = ntl * p.batch;
+
+  // ---- S image fill (as conv_res_pair) ----
+  f32x4 pf[NIT][2];
+  auto issue_fill_item = [&](const float* src, int r0, int k) {
+    const int it = min(tid + 512 * k, NS * G8 - 1);
+    const int s = ((it >> 3) / G8) * 8 + (it & 7), g8 = (it >> 3) % G8;
+    const int a = min(max(r0 - 8 - G::H1 + s, 0), L - 1);
+    const f32x4* q = reinterpret_cast<const f32x4*>(src + (long long)a * C + g8 * 8);
+    pf[k][0] = q[0];
+    pf[k][1] = q[1];
+  };
+  auto commit_fill = [&](int r0) {
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int it = tid + 512 * k;
+      if (!(NIT * 512 == NS * G8 || it < NS * G8)) continue;
+      const int s = ((it >> 3) / G8) * 8 + (it & 7), g8 = (it >> 3) % G8;
+      const int a = r0 - 8 - G::H1 + s;
+      const bool ok = a >= 0 && a < L;
+      s16x8 hv, mv, lv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sv = rp_silu(pf[k][e >> 2][e & 3]);
+        const float v = ok ? sv : 0.f;
+        unsigned short h, m, l;
+        split3(v, h, m, l);
+        hv[e] = (short)h;
+        mv[e] = (short)m;
+        lv[e] = (short)l;
+      }
+      char* d = lds + (s >> 4) * BLK + (g8 >> 1) * 1536 + (g8 & 1) * 768 + (s & 15) * 16;
+      *reinterpret_cast<s16x8*>(d) = hv;
+      *reinterpret_cast<s16x8*>(d + 256) = mv;
+      *reinterpret_cast<s16x8*>(d + 512) = lv;
+    }
+  };
+
+  // ---- weight fragments of chunk ch of a tap ([chunk][Cout][96 B], the ConvParams::w6 tap slice):
+  // [column block][{h',m'} | {h',l'}] ----
+  s16x8 wf[NCH][2][2];
+  auto load_wf = [&](const unsigned short* wtap, int ch) {
+    const char* wb = reinterpret_cast<const char*>(wtap);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const char* w = wb + (ch * C + (2 * wc + cb) * 16 + l15) * 96 + hf * 48;
+      wf[ch][cb][0] = *reinterpret_cast<const s16x8*>(w + t * 16);
+      wf[ch][cb][1] = *reinterpret_cast<const s16x8*>(w + (t ? 32 : 0));
+    }
+  };
+  // the tap after tap j of conv `conv` of member m: the stream runs c1, c2 of each member, then
+  // member 0 again (the next tile; past the last tile harmless loads of weights already used)
+  auto next_tap = [&](int m, int conv, int j) -> const unsigned short* {
+    if (j + 1 < p.taps[m]) return (conv ? p.w2[m] : p.w1[m]) + (long long)(j + 1) * (WTAP / 2);
+    if (conv == 0) return p.w2[m];
+    return p.w1[m + 1 < nmem ? m + 1 : 0];
+  };
+
+  // ---- one tap, chunk-major: the MFMAs of chunk ch for every row block of the wave, then chunk ch
+  // of the next tap into the fragment registers; hook() once every reload of the tap is issued (its
+  // loads are then younger than the fragments the next tap waits for) ----
+  const int soX0 = (hf * 3 + t) * 256, soX1 = (hf * 3 + (t ? 0 : 1)) * 256, soX2 = (hf * 3 + (t ? 0 : 2)) * 256;
+  auto tap = [&](f32x4 (&acc)[RB][2], int rowoff, int nrb, const unsigned short* wnext, auto hook) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        if (i < nrb) {
+          const int sr = (wr + WR * i) * 16 + l15 + rowoff;
+          const char* xr = lds + (sr >> 4) * BLK + (sr & 15) * 16 + ch * 1536;
+          const s16x8 x2 = *reinterpret_cast<const s16x8*>(xr + soX2);
+          const s16x8 x1 = *reinterpret_cast<const s16x8*>(xr + soX1);
+          const s16x8 x0 = *reinterpret_cast<const s16x8*>(xr + soX0);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) {
+            acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][1]),
+                                                                 __builtin_bit_cast(bf16x8, x2), acc[i][cb], 0, 0, 0);
+            acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][0]),
+                                                                 __builtin_bit_cast(bf16x8, x1), acc[i][cb], 0, 0, 0);
+            acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][0]),
+                                                                 __builtin_bit_cast(bf16x8, x0), acc[i][cb], 0, 0, 0);
+          }
+        }
+      }
+      load_wf(wnext, ch);
+      // keep the reloads here: left to itself the scheduler sinks all of them to the end of the tap,
+      // and the next tap's first MFMAs then wait a whole L2 round trip
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    hook();
+  };
+  auto no_hook = [] {};
+
+  const int nrb2 = min(RB, (G::NB2 - wr + WR - 1) / WR);
+  int tile = blockIdx.x;
+  if (tile >= total) return;  // whole workgroup, before any barrier
+  int b = tile / ntl, r0 = (tile - b * ntl) * R;
+  if (tid < 2 * nmem * C) {
+    const int conv = tid / (nmem * C), m = (tid / C) % nmem, c = tid % C;
+    bias_lds[(conv * kMaxGroup + m) * C + c] = (conv ? p.b2[m] : p.b1[m])[c];
+  }
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) load_wf(p.w1[0], ch);
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) issue_fill_item(p.src[0] + (long long)b * p.bstride, r0, k);
+  commit_fill(r0);
+  rp_barrier();
+  f32x4 macc[MEAN ? RB : 1][2];
+#ifdef RP_DIAG_STAMPS
+  unsigned long long dg[16] = {};
+#endif
+  for (;;) {
+    const int next_tile = tile + gridDim.x;
+    const bool more = next_tile < total;
+    const int nb = more ? next_tile / ntl : 0, nr0 = more ? (next_tile - nb * ntl) * R : 0;
+    for (int m = 0; m < nmem; ++m) {
+      const int k = p.taps[m], hk = (k - 1) >> 1, d = p.dil[m];
+      const long long cb0 = (long long)b * p.bstride;
+      const bool last_m = m + 1 == nmem;
+      const bool has_next = !last_m || more;
+      f32x4 acc[RB][2];
+      RP_T(ta);
+      // ---- c1 over rows [r0 - 8, r0 + R + 8) from the S image
+#pragma unroll
+      for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < k; ++j) tap(acc, G::H1 + (j - hk) * d, RB, next_tap(m, 0, j), no_hook);
+      RP_T(tb);
+      rp_barrier();  // every wave's S reads are done before T overwrites them
+      // ---- T image: silu(c1 + b1) planes over the S image (zero outside the clip)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(bias_lds + m * C + c0);
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int ir = (wr + WR * i) * 16 + l15, a = r0 - 8 + ir;
+          const bool ok = a >= 0 && a < L;
+          s16x4 hv, mv, lv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float sv = rp_silu(acc[i][cb][e] + bias[e]);
+            const float v = ok ? sv : 0.f;
+            unsigned short h, mm, l;
+            split3(v, h, mm, l);
+            hv[e] = (short)h;
+            mv[e] = (short)mm;
+            lv[e] = (short)l;
+          }
+          char* dst = lds + (ir >> 4) * BLK + (c0 >> 4) * 1536 + ((c0 >> 3) & 1) * 768 + (ir & 15) * 16 + (c0 & 7) * 2;
+          *reinterpret_cast<s16x4*>(dst) = hv;
+          *reinterpret_cast<s16x4*>(dst + 256) = mv;
+          *reinterpret_cast<s16x4*>(dst + 512) = lv;
+        }
+      }
+      rp_barrier();
+      RP_T(tc);
+      // ---- c2 over rows [r0, r0 + R) from the T image.  Tap 0 loads the residual rows, taps 1 and 2
+      // the next S image's rows (this tile's next ResBlock, or the next tile's first), each after the
+      // tap's fragment reloads (k >= 3, so taps 0..2 exist; they are peeled so that the register
+      // arrays are indexed by constants)
+#pragma unroll
+      for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* nsrc = !last_m ? p.src[m + 1] + cb0 : p.src[0] + (long long)nb * p.bstride;
+      const int nsr0 = !last_m ? r0 : nr0;
+      f32x4 res[RB][2];
+      auto res_hook = [&] {
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int q = min(r0 + (wr + WR * i) * 16 + l15, L - 1);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) {
+            const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+            res[i][cb] = *reinterpret_cast<const f32x4*>(p.src[m] + cb0 + (long long)q * C + c0);
+          }
+        }
+      };
+      auto pf_hook0 = [&] {
+        if (!has_next) return;
+#pragma unroll
+        for (int kk = 0; kk < NIT / 2; ++kk) issue_fill_item(nsrc, nsr0, kk);
+      };
+      auto pf_hook1 = [&] {
+        if (!has_next) return;
+#pragma unroll
+        for (int kk = NIT / 2; kk < NIT; ++kk) issue_fill_item(nsrc, nsr0, kk);
+      };
+      tap(acc, 8 - hk, nrb2, next_tap(m, 1, 0), res_hook);
+      tap(acc, 9 - hk, nrb2, next_tap(m, 1, 1), pf_hook0);
+      tap(acc, 10 - hk, nrb2, next_tap(m, 1, 2), pf_hook1);
+      for (int j = 3; j < k; ++j) tap(acc, 8 + j - hk, nrb2, next_tap(m, 1, j), no_hook);
+      RP_T(te);
+      // ---- epilogue: state + c2 + b2 (rows past the clip end are dropped)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(bias_lds + (kMaxGroup + m) * C + c0);
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          if (i >= nrb2) break;
+          const int q = r0 + (wr + WR * i) * 16 + l15;
+          const f32x4 v = res[i][cb] + (acc[i][cb] + bias);
+          if constexpr (!MEAN) {
+            if (q < L) *reinterpret_cast<f32x4*>(p.dst[m] + cb0 + (long long)q * C + c0) = v;
+          } else if (m == 0) {
+            macc[i][cb] = v;
+          } else if (!last_m) {
+            macc[i][cb] = macc[i][cb] + v;
+          } else {
+            const f32x4 mv = (macc[i][cb] + v) / 3.0f;
+            f32x4 sv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sv[e] = rp_silu(mv[e]);
+            if (q < L) *reinterpret_cast<f32x4*>(p.mean_out + cb0 + (long long)q * C + c0) = sv;
+          }
+        }
+      }
+      RP_T(tf);
+      if (has_next) {
+        rp_barrier();  // every wave's T reads are done before the next S image overwrites them
+        commit_fill(nsr0);
+        rp_barrier();
+      }
+#ifdef RP_DIAG_STAMPS
+      {
+        RP_T(tg);
+        dg[0] += tb - ta; dg[1] += tc - tb; dg[2] += te - tc; dg[3] += tf - te; dg[4] += tg - tf;
+        dg[5] += 1; dg[6] += k; dg[7] += k;
+      }
+#endif
+    }
+    if (!more) break;
+    tile = next_tile;
+    b = nb;
+    r0 = nr0;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last tap's (unused) fragment reloads
+#ifdef RP_DIAG_STAMPS
+  if (tid == 0)
+    for (int i = 0; i < 16; ++i) atomicAdd(&g_rp_diag[(C == 64 ? 16 : 0) + i], dg[i]);
+#endif
+}
 #ifdef RP_DIAG_STAMPS
 extern "C" int dcx_diag_rp(unsigned long long* out32, int reset) {
   if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_rp_diag), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
@@ -424,6 +700,17 @@ hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** k
       return hipErrorInvalidValue;
   }
   const unsigned grid = (unsigned)std::min<long long>(total, cus);  // one workgroup per CU (LDS)
+  // C = 32: the barrier-free kernel (A/B in one session: 12.4 vs 12.9 ms per C2 generator);
+  // C = 64: the step schedule, which measured faster there (22.3 vs 23.2 ms).
+  // DCX_RP_OLD=1 (read at each launch; A/B and tests) runs the step schedule at C = 32 too.
+  const char* oe = getenv("DCX_RP_OLD");
+  const bool old = oe && *oe && *oe != '0';
+  if (p.C == 32 && !old) {
+    if (kname) *kname = p.mean_out ? "conv_res_pair_g<32,mean>" : "conv_res_pair_g<32>";
+    if (p.mean_out) hipLaunchKernelGGL((conv_res_pair_g<32, true>), dim3(grid), dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((conv_res_pair_g<32, false>), dim3(grid), dim3(512), 0, s, p);
+    return hipGetLastError();
+  }
   if (p.C == 32) {
     if (kname) *kname = p.mean_out ? "conv_res_pair<32,mean>" : "conv_res_pair<32>";
     if (p.mean_out) hipLaunchKernelGGL((conv_res_pair<32, true>), dim3(grid), dim3(512), 0, s, p);

@@ -76,3 +76,22 @@ def test_fused_batch_invariance(engines):
     for i in range(3):
         one = fused.generate(z[i: i + 1])
         assert torch.equal(one[0], full[i])
+
+
+@pytest.mark.parametrize("B,T", [(1, 1), (2, 7), (3, 40), (8, 200)])
+def test_unit_pipeline_same_bits_as_step_schedule(engines, B, T):
+    """conv_res_pair_g (barrier-free tap loops, fragments loaded from L2 a tap ahead; the C = 32 stage) against the round-2 step
+    schedule (DCX_RP_OLD=1, read at each launch): the same MFMAs in the same order, so the same bits,
+    also over many tiles per workgroup (B=8, T=200: the persistent tile loop and the ring's
+    wrap-around past the last tile)."""
+    fused, _ = engines
+    z = _z(B, T, 300 + T)
+    a = fused.generate(z)
+    os.environ["DCX_RP_OLD"] = "1"
+    try:
+        b = fused.generate(z)
+    finally:
+        del os.environ["DCX_RP_OLD"]
+    torch.cuda.synchronize()
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b)
