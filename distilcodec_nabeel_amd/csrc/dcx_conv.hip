@@ -2190,6 +2190,14 @@ static hipError_t launch_x6dq(const ConvParams& p, int batch, int phases, hipStr
 // in MEM1(t - 2) and retired one memory segment later.  LDS images: 16-row blocks, piece-major
 // (16-byte unit (r >> 4) * 64 + piece * 16 + (r & 15), piece = 8-channel group of the step).
 // ---------------------------------------------------------------------------------------------
+//
+// REG (round 3): the pwconv1 launches (GELU, compact bf16 output only) swap the MFMA operands, so a
+// lane's 16x16 accumulator holds 4 consecutive output channels of one row, and finish the tile
+// straight from registers (bias, GELU, 8-byte compact stores): no LDS staging, no barriers.  These
+// launches spent 24 us per tile in the LDS-staged epilogue against 8 us in their K loop (C = 256).
+// The swap transposes each 16x16 product (the same K products summed per element), so the bits
+// are those of the staged epilogue.
+template <bool REG>
 __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
   DCX_TILET(tile_t0);
   constexpr int BM = 256, BN = 256, WN = 2, WM = 4;
@@ -2273,8 +2281,12 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
-                                                            __builtin_bit_cast(bf16x8, bq[j]), acc[i][j], 0, 0, 0);
+        if constexpr (REG)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bq[j]),
+                                                              __builtin_bit_cast(bf16x8, af[i]), acc[i][j], 0, 0, 0);
+        else
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                              __builtin_bit_cast(bf16x8, bq[j]), acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
   auto inc3 = [](int& slot) { slot = slot == 2 ? 0 : slot + 1; };
@@ -2325,7 +2337,28 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
   }
 #endif
   DCX_TILET(tile_t2);
-  epilogue_lds<BM, BN, WM, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+  if constexpr (REG) {
+    // lane l of block (i, j): output channels co0 + wn*WC + 16 j + 4 (l >> 4) + e of row 16 i + (l & 15)
+    // of the wave's rows; bias, bf16 rounding, GELU, RNE store (epilogue_lds's operations and order)
+    unsigned short* const y6 = p.y6 + (long long)b * p.y_bstride;
+    const int cq = wn * WC + 4 * (lane >> 4);
+    f32x4 bias[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      bias[j] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co0 + cq + 16 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int q = q0 + wm * WR + 16 * i + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const f32x4 x = round_bf16x4(acc[i][j] + bias[j]);
+        const f32x2 g0 = gelu_bf16_f2(f32x2{x[0], x[1]}), g1 = gelu_bf16_f2(f32x2{x[2], x[3]});
+        if (q < p.Lq) store_bf16x4(y6, q, p.Cout, co0 + cq + 16 * j, g0[0], g0[1], g1[0], g1[1]);
+      }
+    }
+  } else {
+    epilogue_lds<BM, BN, WM, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+  }
 #ifdef DCX_TILE_DIAG
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -3316,6 +3349,12 @@ hipError_t launch_splitk_epilogue(const ConvParams& p, const float* partials, in
   return hipGetLastError();
 }
 
+// DCX_BF16_REG_EPI=0 (read at each launch; A/B and tests): the LDS-staged epilogue for pwconv1 too
+static bool reg_epi_off() {
+  const char* e = getenv("DCX_BF16_REG_EPI");
+  return e && *e == '0';
+}
+
 bool bf16dm_takes(int cin, int cout, int lq, int ldx, int phases) {
 #ifdef DCX_NO_BF16DM
   return false;
@@ -3374,12 +3413,16 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
     if (p.x_compact && (!dm_b1 || p.x_compact != 1)) return hipErrorInvalidValue;  // only conv_gemm_bf16dm reads it
 #ifndef DCX_NO_BF16DM
     if (dm_b1) {
-      if (kname) *kname = "conv_gemm_bf16dm<256,256>";
       ConvParams q = p;
       q.batch = batch;
       q.phases = phases;
-      hipLaunchKernelGGL(conv_gemm_bf16dm, dim3((unsigned)(((p.Lq + 255) / 256) * (p.Cout / 256) * batch * phases)), dim3(512), 0,
-                         s, q);
+      const dim3 grid((unsigned)(((p.Lq + 255) / 256) * (p.Cout / 256) * batch * phases));
+      // pwconv1 (GELU, compact bf16 output only): the register epilogue
+      const bool reg = p.epi == EPI_GELU && p.round_bf16 && p.y6 && p.y_compact == 1 && !p.y && !p.y2 && !p.y6s &&
+                       p.mean_mode == MEAN_NONE && phases == 1 && p.out_mul == 1 && !reg_epi_off();
+      if (kname) *kname = reg ? "conv_gemm_bf16dm<256,256,reg>" : "conv_gemm_bf16dm<256,256>";
+      if (reg) hipLaunchKernelGGL(conv_gemm_bf16dm<true>, grid, dim3(512), 0, s, q);
+      else hipLaunchKernelGGL(conv_gemm_bf16dm<false>, grid, dim3(512), 0, s, q);
       return hipGetLastError();
     }
 #endif

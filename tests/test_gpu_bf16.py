@@ -148,3 +148,31 @@ def test_compact_layout_same_bits(beng, cfg, state, B, secs):
         outs.append((feat, codes, pin, q))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_register_epilogue_same_bits(beng):
+    """conv_gemm_bf16dm's register epilogue for the pwconv1 launches (MFMA operands swapped, bias +
+    GELU + compact stores from the accumulators) against the LDS-staged epilogue
+    (DCX_BF16_REG_EPI=0, read at each launch): encoder features, x_pjt_in and codes bit for bit on a
+    batch that puts every 1x1 conv on conv_gemm_bf16dm (4 x 11 s)."""
+    import os
+
+    from distilcodec_nabeel_amd import synth
+
+    n = 24000 * 11
+    audio = torch.zeros(4, n + 1)
+    for i, c in enumerate(synth.clips(4, n, seed=12, kind="mix")):
+        audio[i, 1:] = torch.from_numpy(c)
+    audio = audio.cuda()
+    outs = []
+    for flag in ("1", "0"):
+        os.environ["DCX_BF16_REG_EPI"] = flag
+        try:
+            feat = beng.encode(beng.mel(audio))
+            codes, pin, _, q = beng.vq_encode(feat, want_fup=False)
+            torch.cuda.synchronize()
+        finally:
+            del os.environ["DCX_BF16_REG_EPI"]
+        outs.append((feat.clone(), codes.clone(), pin.clone(), q.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -31,8 +31,8 @@ def short(name):
     if base == "conv_gemm_x6dm":  # <HALO, BN>: BM = 65536 / BN
         bm, bn = 65536 // int(parts[1]), int(parts[1])
         return f"{base}<{bm},{bn},halo>" if parts[0] != "0" else f"{base}<{bm},{bn}>"
-    if base == "conv_gemm_bf16dm":
-        return "conv_gemm_bf16dm<256,256>"
+    if base == "conv_gemm_bf16dm":  # <REG>
+        return "conv_gemm_bf16dm<256,256,reg>" if parts and parts[0] == "true" else "conv_gemm_bf16dm<256,256>"
     if base == "conv_gemm_x6dq_group":  # <BN>, halo
         return f"{base}<{65536 // int(parts[0])},{parts[0]},halo>"
     if base == "conv_gemm_x6dq":  # <BN>, halo
