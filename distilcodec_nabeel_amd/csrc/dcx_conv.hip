@@ -2191,10 +2191,11 @@ static hipError_t launch_x6dq(const ConvParams& p, int batch, int phases, hipStr
 // (16-byte unit (r >> 4) * 64 + piece * 16 + (r & 15), piece = 8-channel group of the step).
 // ---------------------------------------------------------------------------------------------
 //
-// REG (round 3): the pwconv1 launches (GELU, compact bf16 output only) swap the MFMA operands, so a
-// lane's 16x16 accumulator holds 4 consecutive output channels of one row, and finish the tile
-// straight from registers (bias, GELU, 8-byte compact stores): no LDS staging, no barriers.  These
-// launches spent 24 us per tile in the LDS-staged epilogue against 8 us in their K loop (C = 256).
+// REG (round 3): launches whose epilogue is bias or GELU with a compact bf16 output only (the
+// encoder's pwconv1) swap the MFMA operands, so a lane's 16x16 accumulator holds 4 consecutive output channels of one row, and
+// finish the tile straight from registers (8-byte compact stores): no LDS
+// staging, no barriers.  The pwconv1 launches had spent 24 us per tile in the LDS-staged epilogue
+// against 8 us in their K loop (C = 256).
 // The swap transposes each 16x16 product (the same K products summed per element), so the bits
 // are those of the staged epilogue.
 template <bool REG>
@@ -2339,21 +2340,31 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
   DCX_TILET(tile_t2);
   if constexpr (REG) {
     // lane l of block (i, j): output channels co0 + wn*WC + 16 j + 4 (l >> 4) + e of row 16 i + (l & 15)
-    // of the wave's rows; bias, bf16 rounding, GELU, RNE store (epilogue_lds's operations and order)
+    // of the wave's rows.  epilogue_lds's operations in its order: bias, bf16 rounding, GELU, the
+    // RNE compact store.
     unsigned short* const y6 = p.y6 + (long long)b * p.y_bstride;
-    const int cq = wn * WC + 4 * (lane >> 4);
+    const int cq = co0 + wn * WC + 4 * (lane >> 4);
     f32x4 bias[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
-      bias[j] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co0 + cq + 16 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
+      bias[j] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + cq + 16 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int q = q0 + wm * WR + 16 * i + (lane & 15);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const f32x4 x = round_bf16x4(acc[i][j] + bias[j]);
-        const f32x2 g0 = gelu_bf16_f2(f32x2{x[0], x[1]}), g1 = gelu_bf16_f2(f32x2{x[2], x[3]});
-        if (q < p.Lq) store_bf16x4(y6, q, p.Cout, co0 + cq + 16 * j, g0[0], g0[1], g1[0], g1[1]);
+        f32x4 x = acc[i][j] + bias[j];
+        if (p.round_bf16) x = round_bf16x4(x);
+        if (p.epi == EPI_GELU) {
+          if (p.round_bf16) {
+            const f32x2 g0 = gelu_bf16_f2(f32x2{x[0], x[1]}), g1 = gelu_bf16_f2(f32x2{x[2], x[3]});
+            x = f32x4{g0[0], g0[1], g1[0], g1[1]};  // (the compact store rounds)
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] = gelu_f(x[e]);
+          }
+        }
+        if (q < p.Lq) store_bf16x4(y6, q, p.Cout, cq + 16 * j, x[0], x[1], x[2], x[3]);
       }
     }
   } else {
@@ -3417,9 +3428,12 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       q.batch = batch;
       q.phases = phases;
       const dim3 grid((unsigned)(((p.Lq + 255) / 256) * (p.Cout / 256) * batch * phases));
-      // pwconv1 (GELU, compact bf16 output only): the register epilogue
-      const bool reg = p.epi == EPI_GELU && p.round_bf16 && p.y6 && p.y_compact == 1 && !p.y && !p.y2 && !p.y6s &&
-                       p.mean_mode == MEAN_NONE && phases == 1 && p.out_mul == 1 && !reg_epi_off();
+      // the register epilogue: bias / GELU epilogues with a compact bf16 output only.  With an fp32
+      // output too (the VQ blocks' 1x1 convs) or a residual (pwconv2) it measured slower than the
+      // staged epilogue, whose 16-byte stores cover 512 contiguous bytes of a row per instruction
+      // (C3 bf16dm, A/B: pwconv1 only 52.5 ms, + the fp32-output convs 55.4, + pwconv2 56.6)
+      const bool reg = (p.epi == EPI_BIAS || p.epi == EPI_GELU) && p.y6 && p.y_compact == 1 && !p.y && !p.y2 &&
+                       !p.y6s && p.mean_mode == MEAN_NONE && phases == 1 && p.out_mul == 1 && !reg_epi_off();
       if (kname) *kname = reg ? "conv_gemm_bf16dm<256,256,reg>" : "conv_gemm_bf16dm<256,256>";
       if (reg) hipLaunchKernelGGL(conv_gemm_bf16dm<true>, grid, dim3(512), 0, s, q);
       else hipLaunchKernelGGL(conv_gemm_bf16dm<false>, grid, dim3(512), 0, s, q);
