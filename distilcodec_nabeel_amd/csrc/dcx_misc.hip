@@ -151,8 +151,98 @@ __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict_
   }
 }
 
+// dwconv_ln_run (round 3): the same per-row arithmetic without the per-workgroup staging.  One
+// wave walks RW consecutive rows of one clip with the 7-row input window in registers (a ring of
+// 7 + D rows: row t + 3 + D is loaded while row t is finished), so each input row is read
+// (RW + 6) / RW times and its load overlaps the previous rows' LayerNorms; the taps sit in LDS
+// (28 KiB at C = 1024).  The tiled kernel above held 22 fp32 rows in LDS per 4-wave workgroup
+// (88 KiB at C = 1024: one workgroup per CU, its loads and its arithmetic never overlapping): C3's
+// 19 launches ran at 3.75 TB/s.  The ring slots are static in the unrolled loop (slot = row mod S).
+template <int NV, int RW, int D>
+__global__ void __launch_bounds__(256) dwconv_ln_run_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                             unsigned short* __restrict__ y6, int y6c,
+                                                             const float* __restrict__ dww, const float* __restrict__ dwb,
+                                                             const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                                             int L, int runs, long long nruns) {
+  constexpr int C = 256 * NV, C4 = C / 4, S = 7 + D;
+  __shared__ f32x4 wsh[7 * C4];
+  for (int i = threadIdx.x; i < 7 * C4; i += 256) wsh[i] = reinterpret_cast<const f32x4*>(dww)[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long run = (long long)blockIdx.x * 4 + wave;
+  if (run >= nruns) return;  // whole wave, after the block's only barrier
+  const int bidx = (int)(run / runs), t0 = (int)(run - (long long)bidx * runs) * RW, t1 = min(t0 + RW, L);
+  const float* xb = x + (long long)bidx * L * C;
+  f32x4 win[S][NV], bv[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) bv[i] = *reinterpret_cast<const f32x4*>(dwb + (lane + 64 * i) * 4);
+  auto load_row = [&](f32x4 (&dst)[NV], int tt) {  // row clamped: out-of-range taps are dropped below
+    const float* src = xb + (long long)min(max(tt, 0), L - 1) * C;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) dst[i] = *reinterpret_cast<const f32x4*>(src + (lane + 64 * i) * 4);
+  };
+  // rows t0 - 3 .. t0 + 2 + D in slots 0 .. 5 + D (row r in slot (r - t0 + 3) mod S)
+#pragma unroll
+  for (int k = 0; k < 6 + D; ++k) load_row(win[k], t0 - 3 + k);
+  for (int t = t0;; t += S) {
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const int tk = t + k;
+      if (tk >= t1) return;  // wave-uniform
+      if (tk + 3 + D < t1 + 3) load_row(win[(k + S - 1) % S], tk + 3 + D);  // into row tk - 4's slot
+      f32x4 v[NV];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c4 = lane + 64 * i;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+          const int tt = tk + j - 3;
+          const f32x4 pr = win[(k + j) % S][i] * wsh[j * C4 + c4];
+          if (tt >= 0 && tt < L) acc += pr;
+        }
+        v[i] = acc + bv[i];
+      }
+      const long long row = (long long)bidx * L + tk;
+      ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y ? y + row * C : nullptr, y6, y6c, row, lane);
+    }
+  }
+}
+
+template <int NV>
+static void launch_dwconv_ln_nv(const float* x, float* y, unsigned short* y6, int y6c, const float* dww,
+                                const float* dwb, const float* lnw, const float* lnb, int batch, int L, int rw,
+                                hipStream_t s) {
+  const int runs = (L + rw - 1) / rw;
+  const long long nruns = (long long)batch * runs;
+  const dim3 grid((unsigned)((nruns + 3) / 4)), block(256);
+  constexpr int D = NV >= 4 ? 1 : 2;  // rows prefetched beyond the window (registers: 2 waves per SIMD at C = 1024)
+  switch (rw) {
+    case 32: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 32, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns); break;
+    case 16: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 16, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns); break;
+    case 8: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 8, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns); break;
+    default: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 4, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns); break;
+  }
+}
+
 hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6c, const float* dww, const float* dwb,
                             const float* lnw, const float* lnb, int batch, int L, int C, hipStream_t s) {
+  const char* oe = getenv("DCX_DWCONV_TILED");  // A/B and tests: the round-2 tiled kernel (same bits)
+  if (!(oe && *oe && *oe != '0')) {
+    // rows per wave: the longest run that still gives >= 2048 waves (8 per CU), at least 4
+    const long long rows = (long long)batch * L;
+    const int rw = rows >= 2048LL * 32 ? 32 : rows >= 2048LL * 16 ? 16 : rows >= 2048LL * 8 ? 8 : 4;
+    if ((long long)batch * ((L + rw - 1) / rw) / 4 >= (1LL << 31)) return hipErrorInvalidValue;
+    switch (C) {
+      case 256: launch_dwconv_ln_nv<1>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, s); break;
+      case 512: launch_dwconv_ln_nv<2>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, s); break;
+      case 768: launch_dwconv_ln_nv<3>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, s); break;
+      case 1024: launch_dwconv_ln_nv<4>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, s); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+
   const bool small = (long long)batch * ((L + 15) / 16) < 512;
   const int R = small ? 4 : 16, tiles = (L + R - 1) / R;
   if ((long long)batch * tiles >= (1LL << 31)) return hipErrorInvalidValue;

@@ -157,3 +157,33 @@ def test_spec_transform_sample_rate(cfg, state):
 def test_unknown_module_raises(eng):
     with pytest.raises(ValueError):
         eng.module("generator.nonexistent", torch.zeros(1, 4, 32).cuda())
+
+
+@pytest.mark.parametrize("gemm", ["x6", "bf16"])
+@pytest.mark.parametrize("B,secs", [(1, 0.3), (2, 3.0), (24, 10.0)])
+def test_dwconv_run_same_bits_as_tiled(cfg, state, gemm, B, secs):
+    """dwconv_ln_run (one wave per run of rows, register window) against the round-2 tiled kernel
+    (DCX_DWCONV_TILED=1, read at each launch): the same per-row arithmetic, so the encoder features
+    are bit-identical, for runs of 4 (short input), 8 / 16 and 32 rows (24 x 10 s: >= 65536 rows
+    per launch), in the x6 and bf16 modes (fp32 / planes / compact outputs)."""
+    import os
+
+    from distilcodec_nabeel_amd import synth
+    from distilcodec_nabeel_amd.engine import NativeCodec
+
+    e = NativeCodec(cfg, {"encoder": state["encoder"], "quantizer": state["quantizer"]}, "cuda:0",
+                    with_generator=False, gemm=gemm)
+    n = int(24000 * secs)
+    audio = torch.zeros(B, n + 1)
+    for i, c in enumerate(synth.clips(B, n, seed=21, kind="mix")):
+        audio[i, 1:] = torch.from_numpy(c)
+    mel = e.mel(audio.cuda())
+    a = e.encode(mel).clone()
+    os.environ["DCX_DWCONV_TILED"] = "1"
+    try:
+        b = e.encode(mel)
+        torch.cuda.synchronize()
+    finally:
+        del os.environ["DCX_DWCONV_TILED"]
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b)
