@@ -2192,12 +2192,11 @@ static hipError_t launch_x6dq(const ConvParams& p, int batch, int phases, hipStr
 // ---------------------------------------------------------------------------------------------
 //
 // REG (round 3): launches whose epilogue is bias or GELU with a compact bf16 output only (the
-// encoder's pwconv1) swap the MFMA operands, so a lane's 16x16 accumulator holds 4 consecutive output channels of one row, and
-// finish the tile straight from registers (8-byte compact stores): no LDS
-// staging, no barriers.  The pwconv1 launches had spent 24 us per tile in the LDS-staged epilogue
-// against 8 us in their K loop (C = 256).
-// The swap transposes each 16x16 product (the same K products summed per element), so the bits
-// are those of the staged epilogue.
+// encoder's pwconv1) swap the MFMA operands, so a lane's 16x16 accumulator holds 4 consecutive
+// output channels of one row, and finish the tile straight from registers (8-byte compact stores):
+// no LDS staging, no barriers.  The pwconv1 launches had spent 24 us per tile in the LDS-staged
+// epilogue against 8 us in their K loop (C = 256).  The swap transposes each 16x16 product (the
+// same K products summed per element), so the bits are those of the staged epilogue.
 template <bool REG>
 __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
   DCX_TILET(tile_t0);
