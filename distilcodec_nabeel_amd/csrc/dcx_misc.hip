@@ -152,12 +152,13 @@ __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict_
 }
 
 // dwconv_ln_run (round 3): the same per-row arithmetic without the per-workgroup staging.  One
-// wave walks RW consecutive rows of one clip with the 7-row input window in registers (a ring of
-// 7 + D rows: row t + 3 + D is loaded while row t is finished), so each input row is read
-// (RW + 6) / RW times and its load overlaps the previous rows' LayerNorms; the taps sit in LDS
-// (28 KiB at C = 1024).  The tiled kernel above held 22 fp32 rows in LDS per 4-wave workgroup
-// (88 KiB at C = 1024: one workgroup per CU, its loads and its arithmetic never overlapping): C3's
-// 19 launches ran at 3.75 TB/s.  The ring slots are static in the unrolled loop (slot = row mod S).
+// wave walks RW consecutive rows of one clip (launches of >= 8192 rows) with the 7-row input
+// window in registers (a ring of 7 + D rows: row t + 3 + D is loaded while row t is finished), so
+// each input row is read (RW + 6) / RW times and its load overlaps the previous rows' LayerNorms;
+// the taps sit in LDS (28 KiB at C = 1024).  The tiled kernel above held 22 fp32 rows in LDS per
+// 4-wave workgroup (88 KiB at C = 1024: one workgroup per CU, its loads and its arithmetic never
+// overlapping): C3's 19 launches ran at 3.75 TB/s.  The ring slots are static in the unrolled loop
+// (slot = row mod S).
 template <int NV, int RW, int D>
 __global__ void __launch_bounds__(256) dwconv_ln_run_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                              unsigned short* __restrict__ y6, int y6c,
@@ -228,9 +229,11 @@ static void launch_dwconv_ln_nv(const float* x, float* y, unsigned short* y6, in
 hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6c, const float* dww, const float* dwb,
                             const float* lnw, const float* lnb, int batch, int L, int C, hipStream_t s) {
   const char* oe = getenv("DCX_DWCONV_TILED");  // A/B and tests: the round-2 tiled kernel (same bits)
-  if (!(oe && *oe && *oe != '0')) {
-    // rows per wave: the longest run that still gives >= 2048 waves (8 per CU), at least 4
-    const long long rows = (long long)batch * L;
+  const long long rows = (long long)batch * L;
+  // below 8192 rows (a streaming hop: 93 rows) the tiled kernel's 4-row tiles, one row per wave,
+  // measured faster than runs of 1 or 4 rows (C5 hop 4.06-4.09 vs 4.09-4.14 ms, A/B)
+  if (!(oe && *oe && *oe != '0') && rows >= 8192) {
+    // rows per wave: the longest run that still gives >= 2048 waves (8 per CU)
     const int rw = rows >= 2048LL * 32 ? 32 : rows >= 2048LL * 16 ? 16 : rows >= 2048LL * 8 ? 8 : 4;
     if ((long long)batch * ((L + rw - 1) / rw) / 4 >= (1LL << 31)) return hipErrorInvalidValue;
     switch (C) {
