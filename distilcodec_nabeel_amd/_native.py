@@ -97,7 +97,8 @@ SIGNATURES = {
     "dcx_conv_forward": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, _P, _P, _P, _I32, _P]),
     "dcx_conv_destroy": (None, [_P]),
     "dcx_module_workspace_size": (_SZ, [_P, ctypes.c_char_p, _I32, _I64]),
-    "dcx_module_forward": (ctypes.c_int, [_P, ctypes.c_char_p, _P, _I32, _I64, _P, _P, _SZ, _P]),
+    "dcx_module_io": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
+    "dcx_module_forward": (ctypes.c_int, [_P, ctypes.c_char_p, _P, _I32, _I64, _I32, _P, _P, _SZ, _P]),
     "dcx_vq_rescore_stats": (ctypes.c_int, [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I32]),
     "dcx_profile_enable": (ctypes.c_int, [_P, _I32]),
     "dcx_profile_reset": (ctypes.c_int, [_P]),
@@ -139,7 +140,7 @@ def lib() -> ctypes.CDLL:
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.dcx_abi_version() != 1:
+    if L.dcx_abi_version() != 2:
         raise NativeUnavailable("libdcx.so ABI version mismatch")
     # A library selected explicitly with DCX_LIB (A/B tooling, diagnostic builds) is taken as is;
     # the in-tree library must have been built from the sources next to it.

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -40,6 +41,7 @@ struct ConvW {
   unsigned short* w6 = nullptr;  // bf16 3-plane split, x6 kernel layout
   unsigned short* wc = nullptr;  // 1x1 convs: hi plane only, [Cin/32][Cout][32] (bf16 mode, conv_gemm_bf16dm)
   float* b = nullptr;
+  float* b16 = nullptr;  // the bias rounded to bf16 (bf16 mode: autocast casts it with the weight)
   int cin = 0, cout = 0, taps = 1, phases = 1, in_step = 1, out_mul = 1;
   int in_base[dcx::kMaxPhases] = {0};
 };
@@ -113,6 +115,8 @@ struct dcx_codec {
   unsigned short* codebook_bk = nullptr;  // hi/mid per K32 step (vq_prefilter_bq / _dm; DCX_VQ_OLD builds)
   unsigned short* codebook_b1 = nullptr;  // [CD/32][NC][32] bf16 hi (vq_prefilter_b1)
   unsigned short* ptable6 = nullptr;  // decode table as activation planes (x6 mode gathers)
+  // bf16-mode decode table (planes; mid = lo = 0): project_out under autocast, bf16(bf16(E) W16^T + b16)
+  unsigned short* ptable6b = nullptr;
   int gemm_mode = DCX_GEMM_X6;
   // fused ResBlock pairs for the C = 32 / 64 generator stages (conv_res_pair); DCX_NO_RESPAIR=1 at
   // dcx_create keeps the per-conv launches (A/B comparisons)
@@ -392,6 +396,14 @@ struct Builder {
     auto t = need(k, {n});
     return t ? upload(t->data) : nullptr;
   }
+  // the same vector rounded to bf16 values (fp32 storage)
+  float* vec_bf16(const std::string& k, int64_t n) {
+    auto t = need(k, {n});
+    if (!t) return nullptr;
+    std::vector<float> r(t->data.size());
+    for (size_t i = 0; i < r.size(); ++i) r[i] = bf16_f(bf16_rne(t->data[i]));
+    return upload(r);
+  }
   HostTensor weight(const std::string& prefix, std::vector<int64_t> shape) {
     HostTensor w;
     if (bad()) return w;
@@ -418,7 +430,10 @@ struct Builder {
     c.w = upload(pk);
     if (cin % 16 == 0) c.w6 = split_pack(pk, 1, cout, k, cin);
     if (k == 1 && cin % 32 == 0) c.wc = compact_pack(pk, cout, cin);
-    if (has_bias) c.b = vec(prefix + ".bias", cout);
+    if (has_bias) {
+      c.b = vec(prefix + ".bias", cout);
+      c.b16 = vec_bf16(prefix + ".bias", cout);
+    }
     return c;
   }
 
@@ -442,6 +457,7 @@ struct Builder {
     c.w = upload(pk);
     if (cin % 16 == 0) c.w6 = split_pack(pk, s, cout, taps, cin);
     c.b = vec(prefix + ".bias", cout);
+    c.b16 = vec_bf16(prefix + ".bias", cout);
     return c;
   }
 
@@ -581,7 +597,8 @@ int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32,
   p.x6 = x6 ? c.x.p : nullptr;
   p.w = w.w;
   p.w6 = x6 ? w.w6 : nullptr;
-  p.bias = w.b;
+  const bool one = x6 && h->gemm_mode == DCX_GEMM_BF16 && !c.exact;
+  p.bias = one && w.b16 ? w.b16 : w.b;  // autocast rounds the bias with the other operands
   p.gamma = c.gamma;
   p.res = c.res;
   p.y = c.y;
@@ -604,7 +621,6 @@ int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32,
   for (int i = 0; i < dcx::kMaxPhases; ++i) p.in_base[i] = w.in_base[i];
   p.epi = c.epi;
   p.mean_mode = c.mean;
-  const bool one = x6 && h->gemm_mode == DCX_GEMM_BF16 && !c.exact;
   p.nprod = one ? 1 : 6;
   p.round_bf16 = one;
   p.silu_in = c.silu_in;
@@ -767,7 +783,8 @@ int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, in
   ln.c1 = ln.p && takes_compact(h, bw.pw1, M);
   hid.c1 = hid.p && takes_compact(h, bw.pw2, M);
   LAUNCH(h, s, "dwconv_ln", 14.0 * M * C, 8.0 * M * C,
-         dcx::launch_dwconv_ln(x, ln.f, ln.p, ln.c1 ? 1 : 0, bw.dww, bw.dwb, bw.ln.w, bw.ln.b, B, T, C, s));
+         dcx::launch_dwconv_ln(x, ln.f, ln.p, ln.c1 ? 1 : 0, bw.dww, bw.dwb, bw.ln.w, bw.ln.b, B, T, C,
+                               h->gemm_mode == DCX_GEMM_BF16 ? 1 : 0, s));
   ConvCall c1 = pointwise(ln, M);
   c1.out_to(hid);
   c1.epi = dcx::EPI_GELU;
@@ -783,9 +800,12 @@ int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, in
   return DCX_OK;
 }
 
-int run_ln(dcx_codec* h, const LnW& l, const float* x, Act y, long long rows, hipStream_t s) {
+// channels-first LayerNorm; bf16_in: its input is a bf16 tensor under the reference's autocast (the
+// stem's, in bf16 mode), so its mean and differences are bf16 (ln_rows form 2)
+int run_ln(dcx_codec* h, const LnW& l, const float* x, Act y, long long rows, hipStream_t s, bool bf16_in = false) {
+  const int form = bf16_in && h->gemm_mode == DCX_GEMM_BF16 ? 2 : 1;
   LAUNCH(h, s, "ln_rows", 8.0 * rows * l.C, 8.0 * rows * l.C,
-         dcx::launch_ln_rows(x, y.f, y.p, y.p && y.c1 ? 1 : 0, l.w, l.b, rows, l.C, 1e-6f, 1, s));
+         dcx::launch_ln_rows(x, y.f, y.p, y.p && y.c1 ? 1 : 0, l.w, l.b, rows, l.C, 1e-6f, form, s));
   return DCX_OK;
 }
 
@@ -832,7 +852,7 @@ int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipSt
   ConvCall cc = framed(mel, B, T, c.n_mels);
   cc.y = xa;
   RUN(run_conv(h, h->stem, cc, s));
-  RUN(run_ln(h, h->stem_ln, xa, Act{xb, nullptr}, M, s));
+  RUN(run_ln(h, h->stem_ln, xa, Act{xb, nullptr}, M, s, /*bf16_in=*/true));
   for (int i = 0; i < 4; ++i) {
     if (i > 0) {
       ln.c1 = ln.p && takes_compact(h, h->ds_conv[i], M);
@@ -886,7 +906,10 @@ VqScratch vq_scratch(const dcx_codec* h, Bump& ws, long long M, int ntiles, bool
     v.xr2 = ws.f((size_t)M);
     v.pv2 = ws.f((size_t)M * ntiles);
     v.x2d = (double*)ws.raw((size_t)M * sizeof(double));
-    v.cap = h->vq_pairs_per_row > 0 ? std::max<long long>((long long)h->vq_pairs_per_row * M, 1024) / 8 * 8 : 0;
+    // list offsets are stored as int (row_list): at most INT_MAX pairs; rows beyond are rescored in place
+    v.cap = h->vq_pairs_per_row > 0
+                ? std::min<long long>(std::max<long long>((long long)h->vq_pairs_per_row * M, 1024), INT_MAX) / 8 * 8
+                : 0;
     v.pairs = (int2*)ws.raw((size_t)v.cap * sizeof(int2));
     v.cdist = (double*)ws.raw((size_t)(v.cap / 8) * sizeof(double));
     v.ccode = ws.i((size_t)(v.cap / 8));
@@ -942,6 +965,11 @@ int run_vq_search(dcx_codec* h, const float* P, const unsigned short* P6, int xl
   return DCX_OK;
 }
 
+// decode table in planes for this mode's gathers: project_out in fp32 (x6) or under autocast (bf16)
+const unsigned short* decode_table6(const dcx_codec* h) {
+  return h->gemm_mode == DCX_GEMM_BF16 && h->ptable6b ? h->ptable6b : h->ptable6;
+}
+
 int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float* pin, float* fup, float* quant,
                     Bump& ws, hipStream_t s) {
   const dcx_config& c = h->cfg;
@@ -977,7 +1005,7 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   if (quant) {
     if (x6)
       LAUNCH(h, s, "gather_rows", 0, 12.0 * M * D,
-             dcx::launch_gather_rows((const float*)h->ptable6, NC, codes, M, D * 3 / 2, (float*)zd.p, nullptr, NC, s));
+             dcx::launch_gather_rows((const float*)decode_table6(h), NC, codes, M, D * 3 / 2, (float*)zd.p, nullptr, NC, s));
     else
       LAUNCH(h, s, "gather_rows", 0, 8.0 * M * D, dcx::launch_gather_rows(h->ptable, NC, codes, M, D, zd.f, nullptr, NC, s));
     ConvCall cu = pointwise(zd, M);
@@ -1001,7 +1029,7 @@ int stage_vq_decode(dcx_codec* h, const int32_t* codes, int B, int T, Act z, int
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for vq_decode");
   if (x6_mode(h))
     LAUNCH(h, s, "gather_rows", 0, 12.0 * M * D,
-           dcx::launch_gather_rows((const float*)h->ptable6, c.codebook_size, codes, M, D * 3 / 2, (float*)zd.p,
+           dcx::launch_gather_rows((const float*)decode_table6(h), c.codebook_size, codes, M, D * 3 / 2, (float*)zd.p,
                                    n_invalid, c.codebook_size, s));
   else
     LAUNCH(h, s, "gather_rows", 0, 8.0 * M * D,
@@ -1204,8 +1232,10 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
     C = Co;
     L = Lo;
   }
+  const bool bf = h->gemm_mode == DCX_GEMM_BF16;
   LAUNCH(h, s, "conv_post_tanh", 2.0 * B * L * C * c.gen_post_k, 4.0 * B * L * (C + 1),
-         dcx::launch_conv_post_tanh(Mx, h->post_w, h->post_b, wav, B, L, C, c.gen_post_k, s));
+         dcx::launch_conv_post_tanh(Mx, h->post_w, bf ? bf16_f(bf16_rne(h->post_b)) : h->post_b, wav, B, L, C,
+                                    c.gen_post_k, bf ? 1 : 0, s));
   return DCX_OK;
 }
 
@@ -1251,6 +1281,44 @@ bool match_idx(const std::string& m, const char* fmt, int* a, int* b = nullptr) 
   return got == want && n == (int)m.size();
 }
 
+// Input / output widths of a module (dcx_module_io): cin, cout (0: int32 codes), output rows per
+// input row.  False for unknown names.
+bool module_io(const dcx_codec* h, const std::string& m, int& cin, int& cout, int& rate) {
+  const dcx_config& c = h->cfg;
+  int a = -1, b = -1;
+  rate = 1;
+  auto set = [&](int i, int o) {
+    cin = i;
+    cout = o;
+    return true;
+  };
+  if (match_idx(m, "encoder.stages.%d.%d%n", &a, &b) && a >= 0 && a < 4 && b >= 0 && b < c.enc_depths[a])
+    return set(c.enc_dims[a], c.enc_dims[a]);
+  if (m == "encoder.downsample_layers.0") return set(c.n_mels, c.enc_dims[0]);
+  if (m == "encoder.downsample_layers.0.1") return set(c.enc_dims[0], c.enc_dims[0]);
+  if (match_idx(m, "encoder.downsample_layers.%d%n", &a) && a >= 1 && a < 4) return set(c.enc_dims[a - 1], c.enc_dims[a]);
+  if (match_idx(m, "encoder.downsample_layers.%d.0%n", &a) && a >= 1 && a < 4) return set(c.enc_dims[a - 1], c.enc_dims[a - 1]);
+  if (m == "encoder.norm") return set(c.enc_dims[3], c.enc_dims[3]);
+  if (m == "quantizer.downsample.0" || m == "quantizer.downsample.0.1" || m == "quantizer.upsample.0" ||
+      m == "quantizer.upsample.0.1")
+    return set(c.vq_dim, c.vq_dim);
+  if (m == "quantizer.grvq.rvqs.0.project_in") return set(c.vq_dim, c.codebook_dim);
+  if (m == "quantizer.search") return set(c.codebook_dim, 0);
+  if (m == "generator.conv_pre") return set(c.vq_dim, c.gen_channels);
+  int ch = c.gen_channels;
+  for (int i = 0; i < c.n_ups; ++i) {
+    if (m == "generator.ups." + std::to_string(i)) {
+      rate = c.up_rates[i];
+      return set(ch, ch / 2);
+    }
+    ch /= 2;
+    if (match_idx(m, "generator.resblocks.%d.blocks.%d%n", &a, &b) && a == i && b >= 0 && b < c.n_res) return set(ch, ch);
+    if (match_idx(m, "generator.resblocks.%d%n", &a) && a == i) return set(ch, ch);
+  }
+  if (m == "generator.conv_post") return set(ch, 1);
+  return false;
+}
+
 // One module of the reference by its state-dict prefix, on the handle's packed weights and through
 // the same launches the stages use.  x / y: channels-last fp32 [B][L][C] (codes int32 [B][L] for
 // "quantizer.search").  See dcx_module_forward in the header for the list.
@@ -1259,6 +1327,53 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
   const long long M = (long long)B * L;
   float* y = static_cast<float*>(yv);
   int a = -1, b = -1;
+  // Sequential stems of the encoder (encoders.py:22-39): conv k7 + channels-first LayerNorm (i = 0),
+  // LayerNorm + 1x1 conv (i >= 1)
+  if (m == "encoder.downsample_layers.0") {
+    CAct in(x, nullptr);
+    RUN(ensure_planes(h, in, M, c.n_mels, ws, s));
+    float* t = ws.f((size_t)M * c.enc_dims[0]);
+    if (ws.dry) return DCX_OK;
+    if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    ConvCall cc = framed(in, B, L, c.n_mels);
+    cc.y = t;
+    RUN(run_conv(h, h->stem, cc, s));
+    return run_ln(h, h->stem_ln, t, Act{y, nullptr}, M, s, /*bf16_in=*/true);
+  }
+  if (match_idx(m, "encoder.downsample_layers.%d%n", &a) && a >= 1 && a < 4) {
+    Act ln = conv_input(h, ws, (size_t)M * c.enc_dims[a - 1]);
+    if (ws.dry) return DCX_OK;
+    if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    ln.c1 = ln.p && takes_compact(h, h->ds_conv[a], M);
+    RUN(run_ln(h, h->ds_ln[a], x, ln, M, s));
+    ConvCall cd = pointwise(ln, M);
+    cd.y = y;
+    return run_conv(h, h->ds_conv[a], cd, s);
+  }
+  // the quantizer's down / up paths (grfvq.py:68-96): conv (k = factor) or ConvT, then a ConvNeXtBlock
+  if (m == "quantizer.downsample.0" || m == "quantizer.upsample.0") {
+    const bool down = m == "quantizer.downsample.0";
+    const int D = c.vq_dim;
+    CAct in(x, nullptr);
+    RUN(ensure_planes(h, in, M, D, ws, s));
+    Act ln = conv_input(h, ws, (size_t)M * D);
+    Act hid = conv_input(h, ws, (size_t)M * 4 * D);
+    if (ws.dry) return DCX_OK;
+    if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    ConvCall cc = pointwise(in, M);
+    cc.y = y;
+    RUN(run_conv(h, down ? h->vq_down : h->vq_up, cc, s));
+    return run_block(h, down ? h->vq_down_blk : h->vq_up_blk, y, nullptr, B, L, ln, hid, s);
+  }
+  if (m == "quantizer.grvq.rvqs.0.project_in") {  // residual_vq.py:152
+    CAct in(x, nullptr);
+    RUN(ensure_planes(h, in, M, c.vq_dim, ws, s));
+    if (ws.dry) return DCX_OK;
+    if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    ConvCall cp = pointwise(in, M);
+    cp.y = y;
+    return run_conv(h, h->vq_pin, cp, s);
+  }
   // ConvNeXtBlock (convnext_utils.py:263-282)
   const BlockW* blk = nullptr;
   if (match_idx(m, "encoder.stages.%d.%d%n", &a, &b) && a >= 0 && a < 4 && b >= 0 && b < (int)h->blocks[a].size())
@@ -1299,6 +1414,28 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
     return run_vq_search(h, x, P6, xl, M, vs, ntiles, static_cast<int32_t*>(yv), s);
   }
   if (!h->has_gen && m.rfind("generator.", 0) == 0) return fail(h, DCX_ERR_STATE, "generator weights were not finalized");
+  if (m == "generator.conv_pre") {  // generators.py:121
+    CAct in(x, nullptr);
+    RUN(ensure_planes(h, in, M, c.vq_dim, ws, s));
+    if (ws.dry) return DCX_OK;
+    if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    ConvCall cc = framed(in, B, L, c.vq_dim);
+    cc.y = y;
+    return run_conv(h, h->conv_pre, cc, s);
+  }
+  if (m == "generator.conv_post") {  // generators.py:141-145: activation_post (SiLU), conv_post, tanh
+    int ch = c.gen_channels;
+    for (int i = 0; i < c.n_ups; ++i) ch /= 2;
+    float* t = ws.f((size_t)M * ch);
+    if (ws.dry) return DCX_OK;
+    if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    LAUNCH(h, s, "silu_act", 0, 8.0 * M * ch, dcx::launch_silu_act(x, t, nullptr, M, ch, s));
+    const bool bf = h->gemm_mode == DCX_GEMM_BF16;
+    LAUNCH(h, s, "conv_post_tanh", 2.0 * M * ch * c.gen_post_k, 4.0 * M * (ch + 1),
+           dcx::launch_conv_post_tanh(t, h->post_w, bf ? bf16_f(bf16_rne(h->post_b)) : h->post_b, y, B, L, ch,
+                                      c.gen_post_k, bf ? 1 : 0, s));
+    return DCX_OK;
+  }
   // ConvTranspose1d (generators.py:118-147, ups[i])
   if (match_idx(m, "generator.ups.%d%n", &a) && a >= 0 && a < c.n_ups) {
     const ConvW& up = h->ups[a];
@@ -1596,6 +1733,26 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
           hipDeviceSynchronize() != hipSuccess)
         return fail(h, DCX_ERR_HIP, "decode-table build failed");
     }
+    // The bf16 mode's table: project_out under the reference's autocast (residual_vq.py:138 inside
+    // distil_codec.py:590), bf16(bf16(E) W_out16^T + b_out16) by the one-product conv on the codebook
+    // planes; row NC = bf16(b_out) (the masked code).  Built in a scratch fp32 table, then split.
+    h->ptable6b = (unsigned short*)B.alloc((size_t)(NC + 1) * D * 3 / 2);
+    if (!B.bad() && !B.dry && h->codebook6) {
+      float* tmp = nullptr;
+      if (hipMalloc(&tmp, sizeof(float) * (size_t)(NC + 1) * D) != hipSuccess) return fail(h, DCX_ERR_OOM, "hipMalloc failed");
+      const int mode = h->gemm_mode;
+      h->gemm_mode = DCX_GEMM_BF16;
+      ConvCall cp = pointwise(CAct(h->codebook, h->codebook6), NC);
+      cp.y = tmp;
+      int rc = run_conv(h, pout, cp, 0);
+      h->gemm_mode = mode;
+      if (rc == DCX_OK &&
+          (hipMemcpy(tmp + (size_t)NC * D, pout.b16, sizeof(float) * D, hipMemcpyDeviceToDevice) != hipSuccess ||
+           dcx::launch_split_planes(tmp, h->ptable6b, NC + 1, D, 0, 0) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+        rc = fail(h, DCX_ERR_HIP, "bf16 decode-table build failed");
+      hipFree(tmp);
+      if (rc != DCX_OK) return rc;
+    }
   }
   // ---- generator ------------------------------------------------------------------------
   if (with_generator) {
@@ -1744,6 +1901,17 @@ int dcx_encode_decode(dcx_codec* h, const float* audio, int32_t batch, int64_t n
   return stage_encode_decode(h, audio, batch, n, codes, wav, ws, s);
 }
 
+int dcx_module_io(const dcx_codec* h, const char* module, int32_t* in_channels, int32_t* out_channels,
+                  int32_t* out_rate) {
+  if (!h || !module) return DCX_ERR_INVALID_ARG;
+  int ci = 0, co = 0, r = 1;
+  if (!module_io(h, module, ci, co, r)) return fail(const_cast<dcx_codec*>(h), DCX_ERR_INVALID_ARG, std::string("unknown module: ") + module);
+  if (in_channels) *in_channels = ci;
+  if (out_channels) *out_channels = co;
+  if (out_rate) *out_rate = r;
+  return DCX_OK;
+}
+
 size_t dcx_module_workspace_size(const dcx_codec* h, const char* module, int32_t batch, int64_t rows) {
   if (!h || !module || batch <= 0 || rows <= 0 || !h->finalized) return 0;
   Bump d(nullptr, 0, true);
@@ -1751,10 +1919,16 @@ size_t dcx_module_workspace_size(const dcx_codec* h, const char* module, int32_t
   return d.off + 4096;
 }
 
-int dcx_module_forward(dcx_codec* h, const char* module, const float* x, int32_t batch, int64_t rows, void* y,
-                       void* workspace, size_t ws_bytes, void* stream) {
+int dcx_module_forward(dcx_codec* h, const char* module, const float* x, int32_t batch, int64_t rows,
+                       int32_t channels, void* y, void* workspace, size_t ws_bytes, void* stream) {
   STAGE_PRE(false);
   if (!module || !x || !y || rows <= 0 || rows > (1 << 30)) return fail(h, DCX_ERR_INVALID_ARG, "bad arguments");
+  int ci = 0, co = 0, r = 1;
+  if (!module_io(h, module, ci, co, r)) return fail(h, DCX_ERR_INVALID_ARG, std::string("unknown module: ") + module);
+  // the kernels read cin channels per row: any other width would be read out of bounds
+  if (channels != ci)
+    return fail(h, DCX_ERR_INVALID_ARG, std::string(module) + " takes " + std::to_string(ci) + " input channels, got " +
+                                            std::to_string(channels));
   return stage_module(h, module, x, batch, (int)rows, y, ws, s);
 }
 

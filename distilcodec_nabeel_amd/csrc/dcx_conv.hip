@@ -61,11 +61,6 @@ struct XRow {
 // v * sigmoid(v) from v_exp_f32 and v_rcp_f32 (each ~1 ulp): 5 instructions instead of the
 // library expf and an IEEE divide; silu(-inf side) -> -0, silu(+large) -> v.
 __device__ __forceinline__ float silu_f(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
-__device__ __forceinline__ f32x4 round_bf16x4(f32x4 v) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) v[e] = bf16_val(bf16_bits(v[e]));
-  return v;
-}
 __device__ __forceinline__ float gelu_f(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f)); }
 // GELU of the bf16 mode, whose result is rounded to bf16 (2^-8 relative) right after: erf from
 // the Chebyshev-fitted erfc of Numerical Recipes (erfcc, relative error < 1.2e-7 everywhere), one
@@ -359,7 +354,10 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
             }
             break;
           case EPI_GAMMA_RES: x[h] = r[k][h] + gamma4[h] * x[h]; break;
-          case EPI_RES: x[h] = r[k][h] + x[h]; break;
+          case EPI_RES:  // bf16 mode: ResBlock1's `xt + x` of two bf16 tensors is bf16
+            x[h] = r[k][h] + x[h];
+            if (p.round_bf16) x[h] = round_bf16x4(x[h]);
+            break;
           case EPI_LOGCLAMP:
 #pragma unroll
             for (int e = 0; e < 4; ++e) x[h][e] = logf(fmaxf(x[h][e], 1e-5f));
@@ -380,7 +378,10 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
         continue;
       } else if (p.mean_mode == MEAN_LAST) {
 #pragma unroll
-        for (int h = 0; h < NH; ++h) x[h] = (m[k][h] + x[h]) / 3.0f;
+        for (int h = 0; h < NH; ++h) {  // bf16 mode: stack(...).mean(0) of bf16 tensors is bf16
+          x[h] = (m[k][h] + x[h]) / 3.0f;
+          if (p.round_bf16) x[h] = round_bf16x4(x[h]);
+        }
       }
       if (p.y) {
 #pragma unroll
@@ -398,7 +399,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
         if (p.y2 || y6s) {
           float sv[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) sv[e] = silu_f(xv[e]);
+          for (int e = 0; e < 8; ++e) sv[e] = p.round_bf16 ? bf16_val(bf16_bits(silu_f(xv[e]))) : silu_f(xv[e]);
           if (p.y2) {
             *reinterpret_cast<f32x4*>(p.y2 + o) = f32x4{sv[0], sv[1], sv[2], sv[3]};
             *reinterpret_cast<f32x4*>(p.y2 + o + 4) = f32x4{sv[4], sv[5], sv[6], sv[7]};
@@ -414,7 +415,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
         if (p.y2 || y6s) {
           f32x4 sv;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) sv[e] = silu_f(x[0][e]);
+          for (int e = 0; e < 4; ++e) sv[e] = p.round_bf16 ? bf16_val(bf16_bits(silu_f(x[0][e]))) : silu_f(x[0][e]);
           if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
           if (y6s) store_planes4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
         }

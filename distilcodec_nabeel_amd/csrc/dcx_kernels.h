@@ -168,11 +168,14 @@ hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows
 // x2 (fp32) and optionally x2d (fp64) |x|^2, xr2 |x - bf16(x)|^2 per row; zero_me (optional) set to 0
 hipError_t launch_row_sqnorm(const float* x, long long rows, int C, float* out, double* x2d, float* xr2,
                              unsigned long long* zero_me, hipStream_t s);
-// y6c: y6 in the compact bf16 layout instead of planes
+// y6c: y6 in the compact bf16 layout instead of planes; channels_first_form: 0 F.layer_norm, 1 the
+// reference's channels_first LayerNorm, 2 the latter on a bf16 input under CUDA autocast
 hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, int y6c, const float* w, const float* b,
                           long long rows, int C, float eps, int channels_first_form, hipStream_t s);
+// bf16: the reference's CUDA autocast (DCX_GEMM_BF16): input, taps and bias rounded to bf16, the
+// depthwise conv's result rounded to bf16, then the fp32 F.layer_norm
 hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6c, const float* dww, const float* dwb,
-                            const float* lnw, const float* lnb, int batch, int L, int C, hipStream_t s);
+                            const float* lnw, const float* lnb, int batch, int L, int C, int bf16, hipStream_t s);
 // x6 codebook planes -> the per-K32 hi/mid layout of vq_prefilter_bk ((dim / 32) * ncodes * 64 bf16)
 hipError_t launch_repack_codebook_bk(const unsigned short* cb6, int ncodes, int dim, unsigned short* out,
                                      hipStream_t s);
@@ -191,7 +194,7 @@ hipError_t launch_split_planes(const float* x, unsigned short* y6, long long row
 hipError_t launch_gather_rows(const float* table, int ntable, const int32_t* idx, long long rows, int width,
                               float* out, int32_t* n_invalid, int masked_row, hipStream_t s);
 hipError_t launch_conv_post_tanh(const float* x, const float* w, float bias, float* out, int batch, int L, int C,
-                                 int k, hipStream_t s);
+                                 int k, int bf16, hipStream_t s);
 hipError_t launch_transpose(const float* in, float* out, int batch, long long rows, long long cols, hipStream_t s);
 hipError_t launch_resample_poly(const float* x, int batch, long long n_in, long long xs, const double* h, int hlen,
                                 int up, int down, long long pre, float* y, long long n_out, long long ys,

@@ -21,6 +21,10 @@ __device__ __forceinline__ float wave_sum(float v) {
 // LayerNorm over the channel axis of each row.  channels_first_form=1 follows the reference's
 // custom channels_first LayerNorm `(x-u)/sqrt(s+eps)*w+b` (convnext_utils.py:208-213);
 // 0 follows F.layer_norm (`(x-u)*rsqrt(s+eps)*w+b`, convnext_utils.py:205).  Biased variance.
+// 2: the channels_first form on a bf16 input under the reference's CUDA autocast (the encoder
+// stem, whose Conv1d returns bf16; DCX_GEMM_BF16): `x.mean(1)` and `x - u` run in bf16 (fp32
+// arithmetic, bf16 results), `.pow(2)` is on autocast's fp32 list, so s is the fp32 mean of the
+// squared bf16 differences and the rest is fp32.
 // One wave per row, NV float4 per lane (C = 256*NV).
 // ---------------------------------------------------------------------------------------------
 template <int NV>
@@ -30,7 +34,13 @@ __device__ __forceinline__ void ln_finish(f32x4 (&v)[NV], int C, float eps, int 
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-  const float mean = wave_sum(s) / (float)C;
+  float mean = wave_sum(s) / (float)C;
+  if (cf == 2) {  // v := bf16(x - bf16(mean)); the fp32 steps below then see u = 0
+    mean = bf16_val(bf16_bits(mean));
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = round_bf16x4(v[i] - mean);
+    mean = 0.f;
+  }
   float sq = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -46,7 +56,7 @@ __device__ __forceinline__ void ln_finish(f32x4 (&v)[NV], int C, float eps, int 
     const f32x4 wv = *reinterpret_cast<const f32x4*>(w + c);
     const f32x4 bv = *reinterpret_cast<const f32x4*>(b + c);
     f32x4 o;
-    if (cf) {
+    if (cf) {  // 1, 2
       o = (v[i] - mean) / den * wv + bv;
     } else {
       o = (v[i] - mean) * rstd * wv + bv;
@@ -99,7 +109,7 @@ __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict_
                                                          unsigned short* __restrict__ y6, int y6c,
                                                          const float* __restrict__ dww, const float* __restrict__ dwb,
                                                          const float* __restrict__ lnw, const float* __restrict__ lnb,
-                                                         int L, int tiles) {
+                                                         int L, int tiles, int bf) {
   constexpr int C = 256 * NV, C4 = C / 4, ROWS = DW_R + 6;
   __shared__ f32x4 tile[ROWS * C4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -115,6 +125,7 @@ __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict_
     const int tt = t0 - 3 + r;
     const bool ok = i < ROWS * C4 && tt >= 0 && tt < L;
     st[k] = ok ? *reinterpret_cast<const f32x4*>(xb + (long long)tt * C + c4 * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (bf) st[k] = round_bf16x4(st[k]);
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
@@ -126,8 +137,12 @@ __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict_
   for (int i = 0; i < NV; ++i) {
     const int c = (lane + 64 * i) * 4;
 #pragma unroll
-    for (int j = 0; j < 7; ++j) wv[i][j] = *reinterpret_cast<const f32x4*>(dww + j * C + c);
+    for (int j = 0; j < 7; ++j) {
+      wv[i][j] = *reinterpret_cast<const f32x4*>(dww + j * C + c);
+      if (bf) wv[i][j] = round_bf16x4(wv[i][j]);
+    }
     bv[i] = *reinterpret_cast<const f32x4*>(dwb + c);
+    if (bf) bv[i] = round_bf16x4(bv[i]);
   }
   __syncthreads();
   for (int rr = wave; rr < DW_R; rr += 4) {
@@ -145,6 +160,7 @@ __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict_
         if (tt >= 0 && tt < L) acc += pr;
       }
       v[i] = acc + bv[i];
+      if (bf) v[i] = round_bf16x4(v[i]);
     }
     const long long row = (long long)bidx * L + t;
     ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y ? y + row * C : nullptr, y6, y6c, row, lane);
@@ -164,10 +180,13 @@ __global__ void __launch_bounds__(256) dwconv_ln_run_kernel(const float* __restr
                                                              unsigned short* __restrict__ y6, int y6c,
                                                              const float* __restrict__ dww, const float* __restrict__ dwb,
                                                              const float* __restrict__ lnw, const float* __restrict__ lnb,
-                                                             int L, int runs, long long nruns) {
+                                                             int L, int runs, long long nruns, int bf) {
   constexpr int C = 256 * NV, C4 = C / 4, S = 7 + D;
   __shared__ f32x4 wsh[7 * C4];
-  for (int i = threadIdx.x; i < 7 * C4; i += 256) wsh[i] = reinterpret_cast<const f32x4*>(dww)[i];
+  for (int i = threadIdx.x; i < 7 * C4; i += 256) {
+    const f32x4 wv = reinterpret_cast<const f32x4*>(dww)[i];
+    wsh[i] = bf ? round_bf16x4(wv) : wv;
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long long run = (long long)blockIdx.x * 4 + wave;
@@ -176,20 +195,34 @@ __global__ void __launch_bounds__(256) dwconv_ln_run_kernel(const float* __restr
   const float* xb = x + (long long)bidx * L * C;
   f32x4 win[S][NV], bv[NV];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) bv[i] = *reinterpret_cast<const f32x4*>(dwb + (lane + 64 * i) * 4);
+  for (int i = 0; i < NV; ++i) {
+    bv[i] = *reinterpret_cast<const f32x4*>(dwb + (lane + 64 * i) * 4);
+    if (bf) bv[i] = round_bf16x4(bv[i]);
+  }
   auto load_row = [&](f32x4 (&dst)[NV], int tt) {  // row clamped: out-of-range taps are dropped below
     const float* src = xb + (long long)min(max(tt, 0), L - 1) * C;
 #pragma unroll
     for (int i = 0; i < NV; ++i) dst[i] = *reinterpret_cast<const f32x4*>(src + (lane + 64 * i) * 4);
   };
+  // bf16 mode: a row is rounded where it is first used (tap 6 of row r - 3), not where it is loaded,
+  // so the prefetch keeps its distance
+  auto round_row = [&](f32x4 (&r)[NV]) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) r[i] = round_bf16x4(r[i]);
+  };
   // rows t0 - 3 .. t0 + 2 + D in slots 0 .. 5 + D (row r in slot (r - t0 + 3) mod S)
 #pragma unroll
   for (int k = 0; k < 6 + D; ++k) load_row(win[k], t0 - 3 + k);
+  if (bf) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) round_row(win[k]);
+  }
   for (int t = t0;; t += S) {
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       const int tk = t + k;
       if (tk >= t1) return;  // wave-uniform
+      if (bf) round_row(win[(k + 6) % S]);  // row tk + 3, first used now
       if (tk + 3 + D < t1 + 3) load_row(win[(k + S - 1) % S], tk + 3 + D);  // into row tk - 4's slot
       f32x4 v[NV];
 #pragma unroll
@@ -203,6 +236,7 @@ __global__ void __launch_bounds__(256) dwconv_ln_run_kernel(const float* __restr
           if (tt >= 0 && tt < L) acc += pr;
         }
         v[i] = acc + bv[i];
+        if (bf) v[i] = round_bf16x4(v[i]);
       }
       const long long row = (long long)bidx * L + tk;
       ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y ? y + row * C : nullptr, y6, y6c, row, lane);
@@ -212,22 +246,22 @@ __global__ void __launch_bounds__(256) dwconv_ln_run_kernel(const float* __restr
 
 template <int NV>
 static void launch_dwconv_ln_nv(const float* x, float* y, unsigned short* y6, int y6c, const float* dww,
-                                const float* dwb, const float* lnw, const float* lnb, int batch, int L, int rw,
+                                const float* dwb, const float* lnw, const float* lnb, int batch, int L, int rw, int bf,
                                 hipStream_t s) {
   const int runs = (L + rw - 1) / rw;
   const long long nruns = (long long)batch * runs;
   const dim3 grid((unsigned)((nruns + 3) / 4)), block(256);
   constexpr int D = NV >= 4 ? 1 : 2;  // rows prefetched beyond the window (registers: 2 waves per SIMD at C = 1024)
   switch (rw) {
-    case 32: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 32, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns); break;
-    case 16: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 16, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns); break;
-    case 8: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 8, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns); break;
-    default: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 4, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns); break;
+    case 32: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 32, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns, bf); break;
+    case 16: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 16, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns, bf); break;
+    case 8: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 8, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns, bf); break;
+    default: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 4, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns, bf); break;
   }
 }
 
 hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6c, const float* dww, const float* dwb,
-                            const float* lnw, const float* lnb, int batch, int L, int C, hipStream_t s) {
+                            const float* lnw, const float* lnb, int batch, int L, int C, int bf16, hipStream_t s) {
   const char* oe = getenv("DCX_DWCONV_TILED");  // A/B and tests: the round-2 tiled kernel (same bits)
   const long long rows = (long long)batch * L;
   // below 8192 rows (a streaming hop: 93 rows) the tiled kernel's 4-row tiles, one row per wave,
@@ -237,10 +271,10 @@ hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6
     const int rw = rows >= 2048LL * 32 ? 32 : rows >= 2048LL * 16 ? 16 : rows >= 2048LL * 8 ? 8 : 4;
     if ((long long)batch * ((L + rw - 1) / rw) / 4 >= (1LL << 31)) return hipErrorInvalidValue;
     switch (C) {
-      case 256: launch_dwconv_ln_nv<1>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, s); break;
-      case 512: launch_dwconv_ln_nv<2>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, s); break;
-      case 768: launch_dwconv_ln_nv<3>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, s); break;
-      case 1024: launch_dwconv_ln_nv<4>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, s); break;
+      case 256: launch_dwconv_ln_nv<1>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, bf16, s); break;
+      case 512: launch_dwconv_ln_nv<2>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, bf16, s); break;
+      case 768: launch_dwconv_ln_nv<3>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, bf16, s); break;
+      case 1024: launch_dwconv_ln_nv<4>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, bf16, s); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -251,14 +285,14 @@ hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6
   if ((long long)batch * tiles >= (1LL << 31)) return hipErrorInvalidValue;
   dim3 grid((unsigned)(batch * tiles)), block(256);
   switch (C) {
-    case 256: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<1, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles);
-      else hipLaunchKernelGGL((dwconv_ln_kernel<1, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
-    case 512: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<2, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles);
-      else hipLaunchKernelGGL((dwconv_ln_kernel<2, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
-    case 768: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<3, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles);
-      else hipLaunchKernelGGL((dwconv_ln_kernel<3, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
-    case 1024: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<4, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles);
-      else hipLaunchKernelGGL((dwconv_ln_kernel<4, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles); break;
+    case 256: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<1, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16);
+      else hipLaunchKernelGGL((dwconv_ln_kernel<1, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16); break;
+    case 512: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<2, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16);
+      else hipLaunchKernelGGL((dwconv_ln_kernel<2, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16); break;
+    case 768: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<3, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16);
+      else hipLaunchKernelGGL((dwconv_ln_kernel<3, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16); break;
+    case 1024: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<4, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16);
+      else hipLaunchKernelGGL((dwconv_ln_kernel<4, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -737,7 +771,7 @@ __global__ void __launch_bounds__(256) vq_pair_reduce_kernel(const int2* __restr
 
 static bool rescore_args_ok(const VqRescoreArgs& a) {
   return a.ntiles >= 1 && a.ntiles <= kMaxVqTiles && a.dim % 256 == 0 && a.dim <= 256 * kMaxVqDimVec && a.rows >= 0 &&
-         a.rows <= (1ll << 31) - 1 && a.cap % kVqChunk == 0 && a.pairs && a.cdist && a.ccode && a.row_list &&
+         a.rows <= (1ll << 31) - 1 && a.cap >= 0 && a.cap <= 0x7fffffffll && a.cap % kVqChunk == 0 && a.pairs && a.cdist && a.ccode && a.row_list &&
          a.npairs && a.x2d && a.e2d;
 }
 
@@ -780,14 +814,16 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restric
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
-  int i = idx[row];
-  if (i == -1 && masked_row >= 0)
-    i = masked_row;
-  else if (i < 0)
-    i += ntable;
-  if ((i < 0 || i >= ntable) && !(masked_row >= 0 && i == masked_row)) {
-    if (lane == 0 && n_invalid) atomicAdd(n_invalid, 1);
-    i = 0;
+  const int raw = idx[row];
+  int i;
+  if (raw == -1 && masked_row >= 0) {
+    i = masked_row;  // only code -1 reads the masked row
+  } else {
+    i = raw < 0 ? raw + ntable : raw;
+    if (i < 0 || i >= ntable) {
+      if (lane == 0 && n_invalid) atomicAdd(n_invalid, 1);
+      i = 0;
+    }
   }
   const float* src = table + (long long)i * width;
   float* dst = out + row * width;
@@ -807,10 +843,13 @@ hipError_t launch_gather_rows(const float* table, int ntable, const int32_t* idx
 // conv_post (C -> 1, kernel k, "same" padding) + tanh (generators.py:141-145).  The input is
 // already silu-activated by the previous stage's epilogue.  Block = 256 output samples; the
 // input rows they touch are staged once in LDS (row stride 36 floats: conflict-free b128 reads).
+// bf: the reference's CUDA autocast (DCX_GEMM_BF16): bf16 operands (input and weights rounded
+// while staging, the caller passes the bias rounded), the conv result rounded to bf16, tanh of it
+// rounded to bf16.
 // ---------------------------------------------------------------------------------------------
 template <int C>
 __global__ void __launch_bounds__(256) conv_post_tanh_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                              float bias, float* __restrict__ out, int L, int k) {
+                                                              float bias, float* __restrict__ out, int L, int k, int bf) {
   constexpr int LD = C + 4;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int pad = (k - 1) / 2;
@@ -825,9 +864,10 @@ __global__ void __launch_bounds__(256) conv_post_tanh_kernel(const float* __rest
     const int t = t0 - pad + r;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (t >= 0 && t < L) v = *reinterpret_cast<const f32x4*>(xb + (long long)t * C + c4 * 4);
+    if (bf) v = round_bf16x4(v);
     *reinterpret_cast<f32x4*>(tile + r * LD + c4 * 4) = v;
   }
-  for (int i = threadIdx.x; i < k * C; i += 256) ws[i] = w[i];
+  for (int i = threadIdx.x; i < k * C; i += 256) ws[i] = bf ? bf16_val(bf16_bits(w[i])) : w[i];
   __syncthreads();
   const int t = t0 + threadIdx.x;
   if (t >= L) return;
@@ -845,16 +885,19 @@ __global__ void __launch_bounds__(256) conv_post_tanh_kernel(const float* __rest
       acc = fmaf(xv.w, wv.w, acc);
     }
   }
-  out[(long long)b * L + t] = tanhf(acc + bias);
+  if (bf)
+    out[(long long)b * L + t] = bf16_val(bf16_bits(tanhf(bf16_val(bf16_bits(acc + bias)))));
+  else
+    out[(long long)b * L + t] = tanhf(acc + bias);
 }
 
 hipError_t launch_conv_post_tanh(const float* x, const float* w, float bias, float* out, int batch, int L, int C, int k,
-                                 hipStream_t s) {
+                                 int bf16, hipStream_t s) {
   dim3 grid((unsigned)((L + 255) / 256), batch);
   const size_t lds = (size_t)((256 + k - 1) * (C + 4) + k * C) * sizeof(float);
   switch (C) {
-    case 32: hipLaunchKernelGGL(conv_post_tanh_kernel<32>, grid, dim3(256), lds, s, x, w, bias, out, L, k); break;
-    case 64: hipLaunchKernelGGL(conv_post_tanh_kernel<64>, grid, dim3(256), lds, s, x, w, bias, out, L, k); break;
+    case 32: hipLaunchKernelGGL(conv_post_tanh_kernel<32>, grid, dim3(256), lds, s, x, w, bias, out, L, k, bf16); break;
+    case 64: hipLaunchKernelGGL(conv_post_tanh_kernel<64>, grid, dim3(256), lds, s, x, w, bias, out, L, k, bf16); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -14,6 +14,14 @@ typedef short s16x4p __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ unsigned short bf16_bits(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
 __device__ __forceinline__ float bf16_val(unsigned short b) { return __uint_as_float((unsigned)b << 16); }
 
+// four fp32 values rounded to bf16 values (the bf16 mode's torch.autocast rounding points)
+typedef float f32x4p __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4p round_bf16x4(f32x4p v) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = bf16_val(bf16_bits(v[e]));
+  return v;
+}
+
 __device__ __forceinline__ void split3(float x, unsigned short& h, unsigned short& m, unsigned short& l) {
   h = bf16_bits(x);
   const float r1 = x - bf16_val(h);

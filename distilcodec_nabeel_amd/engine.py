@@ -209,26 +209,32 @@ class NativeCodec:
                                                  ws.numel(), self._stream()))
         return codes, wav
 
+    def module_io(self, name: str) -> tuple[int, int, int]:
+        """(input channels, output channels (0: int32 codes), output rows per input row) of a module."""
+        ci, co, r = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        self._check(self.L.dcx_module_io(self.h, name.encode(), ctypes.byref(ci), ctypes.byref(co), ctypes.byref(r)))
+        return ci.value, co.value, r.value
+
     def module(self, name: str, x: torch.Tensor) -> torch.Tensor:
         """One reference module by its state-dict prefix (dcx_module_forward): x channels-last
-        (B, L, C) fp32 -> y (see the header for shapes; int32 codes for "quantizer.search")."""
+        (B, L, C) fp32 -> y (see the header for shapes; int32 codes for "quantizer.search").
+        ValueError for an unknown name or an input whose channel count is not the module's."""
+        cin, cout, rate = self.module_io(name)
         x = self._dev(x, torch.float32)
+        if x.ndim != 3 or x.shape[2] != cin:
+            raise ValueError(f"{name} takes (B, L, {cin}) input, got {tuple(x.shape)}")
         B, L, C = x.shape
         n = name.encode()
         need = int(self.L.dcx_module_workspace_size(self.h, n, B, L))
         if need == 0:
-            raise ValueError(f"unknown module {name!r}")
-        if name == "quantizer.search":
+            raise ValueError(f"module {name!r} cannot run on this handle")
+        if cout == 0:
             y = torch.empty(B, L, dtype=torch.int32, device=self.device)
-        elif name.startswith("generator.ups."):
-            i = int(name.split(".")[2])
-            d = self.cfg["decoder"]
-            y = torch.empty(B, L * d["upsample_rates"][i], d["upsample_initial_channel"] // 2 ** (i + 1), device=self.device)
         else:
-            y = torch.empty(B, L, C, device=self.device)
+            y = torch.empty(B, L * rate, cout, device=self.device)
         ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         with torch.cuda.device(self.device):
-            self._check(self.L.dcx_module_forward(self.h, n, self._ptr(x), B, L, self._ptr(y), self._ptr(ws), ws.numel(),
+            self._check(self.L.dcx_module_forward(self.h, n, self._ptr(x), B, L, C, self._ptr(y), self._ptr(ws), ws.numel(),
                                                   self._stream()))
         return y
 

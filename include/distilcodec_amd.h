@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define DCX_ABI_VERSION 1
+#define DCX_ABI_VERSION 2
 
 enum {
   DCX_OK = 0,
@@ -207,25 +207,37 @@ int dcx_conv_forward(dcx_conv* c, int32_t gemm_mode, const float* x, int32_t bat
 void dcx_conv_destroy(dcx_conv* c);
 
 /* Single reference modules, for per-module parity tests (tests/test_gpu_modules.py against the
- * reference's own module outputs, tests/golden/modules.npz).  `module` is the module's state-dict
- * prefix in the reference; the call runs it on the handle's packed weights through the same kernels
- * and launch code the stages use, in the handle's arithmetic mode.  x / y are channels-last fp32
- * [B][rows][C] unless noted:
+ * reference's own module outputs, tests/golden/modules.npz and bf16.npz).  `module` is the module's
+ * state-dict prefix in the reference; the call runs it on the handle's packed weights through the same
+ * kernels and launch code the stages use, in the handle's arithmetic mode (DCX_GEMM_BF16: the dtypes of
+ * the reference's CUDA autocast).  x / y are channels-last fp32 [B][rows][C] unless noted:
+ *   "encoder.downsample_layers.0": stem Conv1d k7 + channels-first LayerNorm; "encoder.downsample_layers.<i>"
+ *       (i >= 1): channels-first LayerNorm + 1x1 Conv1d (encoders.py:22-39);
  *   "encoder.stages.<i>.<j>", "quantizer.downsample.0.1", "quantizer.upsample.0.1": ConvNeXtBlock
  *       (convnext_utils.py:263-282);
  *   "encoder.downsample_layers.0.1", "encoder.downsample_layers.<i>.0", "encoder.norm": channels-first
  *       LayerNorm (convnext_utils.py:186-213);
+ *   "quantizer.downsample.0" / "quantizer.upsample.0": Conv1d / ConvTranspose1d + ConvNeXtBlock
+ *       (grfvq.py:68-96); "quantizer.grvq.rvqs.0.project_in": Linear (residual_vq.py:152);
+ *   "generator.conv_pre": Conv1d (generators.py:121);
  *   "generator.ups.<i>": ConvTranspose1d, y [B][rows * rate][Cout] (generators.py:29-116);
  *   "generator.resblocks.<i>.blocks.<j>": ResBlock1 (convnext_utils.py:106-113), per-conv launches;
  *   "generator.resblocks.<i>": the stage's ParralelBlock (convnext_utils.py:137-138) as the generator
  *       runs it, with the SiLU that follows it fused: y = silu(mean of the ResBlock1s) (fused pair
  *       kernels at C = 32 / 64);
+ *   "generator.conv_post": the generator's tail, SiLU -> conv_post -> tanh (generators.py:141-145),
+ *       y [B][rows][1];
  *   "quantizer.search": nearest code (vector_quantize_pytorch.py:41-45, 496-506) of x_pjt_in rows
  *       x [B][rows][codebook_dim]; y = int32 codes [B][rows] (x6 and fp32 modes).
- * Unknown names return DCX_ERR_INVALID_ARG.  dcx_module_workspace_size returns 0 for them. */
+ * dcx_module_io reports a module's input channels, output channels (0: int32 codes) and output rows
+ * per input row; unknown names return DCX_ERR_INVALID_ARG (and dcx_module_workspace_size 0).
+ * dcx_module_forward takes the input's channel count and returns DCX_ERR_INVALID_ARG unless it is the
+ * module's (the kernels read that many channels per row). */
+int dcx_module_io(const dcx_codec* h, const char* module, int32_t* in_channels, int32_t* out_channels,
+                  int32_t* out_rate);
 size_t dcx_module_workspace_size(const dcx_codec* h, const char* module, int32_t batch, int64_t rows);
-int dcx_module_forward(dcx_codec* h, const char* module, const float* x, int32_t batch, int64_t rows, void* y,
-                       void* workspace, size_t ws_bytes, void* stream);
+int dcx_module_forward(dcx_codec* h, const char* module, const float* x, int32_t batch, int64_t rows,
+                       int32_t channels, void* y, void* workspace, size_t ws_bytes, void* stream);
 
 /* VQ search diagnostics (x6 / bf16 mode): the search is a bf16 prefilter whose winner is certified
  * by a rigorous error bound; rows with more than one code inside the bound are rescored in fp64.

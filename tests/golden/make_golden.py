@@ -23,6 +23,10 @@ Fixtures
                       each ConvTranspose1d of the generator, EuclideanCodebook search on a
                       1024-code slice, `quantizer.decode` of codes holding the masked code -1,
                       and `spec_transform(..., return_linear=True)` of e2e_batch clip 0.
+* `bf16.npz`        : the reference with `enable_bfloat16=True`, i.e. under CUDA autocast's op policy
+                      applied on the CPU (`_autocast_cuda.py`): e2e features / x_pjt_in / codes / decode
+                      of the e2e_batch clips and per-module cases (see `make_bf16`).
+                      `python tests/golden/make_golden.py bf16` regenerates it alone.
 """
 from __future__ import annotations
 
@@ -169,9 +173,164 @@ def main():
         mods["linear_mel"], mods["linear_log"] = _np(mel_l), _np(lin_l)
     np.savez_compressed(os.path.join(HERE, "modules.npz"), **mods)
     print("modules", sorted(mods))
-    for f in ("e2e_batch.npz", "e2e_3s.npz", "e2e_real.npz", "modules.npz"):
+    make_bf16(codec, out["audio"])
+    for f in ("e2e_batch.npz", "e2e_3s.npz", "e2e_real.npz", "modules.npz", "bf16.npz"):
         print(f, os.path.getsize(os.path.join(HERE, f)) // 1024, "KiB")
 
 
+# ---- enable_bfloat16=True: the reference under CUDA autocast's dtypes ------------------------------
+def _bits(t):
+    """A bf16 tensor as its raw 16-bit patterns (exact, half the bytes of fp32)."""
+    assert t.dtype == torch.bfloat16, t.dtype
+    return _np(t.contiguous().view(torch.int16)).view(np.uint16)
+
+
+def _store(d, key, t):
+    if t.dtype == torch.bfloat16:
+        d[key + "_bf16"] = _bits(t)
+    else:
+        d[key] = _np(t.float())
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
+
+
+# the encoder / quantizer modules see rows [0, ENC_ROWS) of clip 0 of e2e_batch as captured, the
+# generator modules the decode of its first GEN_FRAMES codes
+ENC_ROWS = 32
+GEN_FRAMES = 8
+
+
+def _bf16_modules(codec):
+    enc, q, g = codec.encoder, codec.quantizer, codec.generator
+    mods = [("encoder.downsample_layers.0", enc.downsample_layers[0])]
+    for i in range(1, 4):
+        mods.append((f"encoder.downsample_layers.{i}", enc.downsample_layers[i]))
+    for i in range(4):
+        mods.append((f"encoder.stages.{i}.0", enc.stages[i][0]))
+    mods += [("encoder.stages.2.4", enc.stages[2][4]),
+             ("quantizer.downsample.0", q.downsample[0]), ("quantizer.grvq.rvqs.0.project_in", q.grvq.rvqs[0].project_in),
+             ("quantizer.upsample.0", q.upsample[0]), ("generator.conv_pre", g.conv_pre)]
+    for i in range(len(g.ups)):
+        mods += [(f"generator.ups.{i}", g.ups[i])]
+        nb = len(g.resblocks[i].blocks) if i >= 3 else 1  # every ResBlock1 of the small-C stages
+        mods += [(f"generator.resblocks.{i}.blocks.{j}", g.resblocks[i].blocks[j]) for j in range(nb)]
+        mods += [(f"generator.resblocks.{i}", g.resblocks[i])]
+    mods.append(("generator.conv_post", g.activation_post))  # input of the tail: SiLU -> conv_post -> tanh
+    return mods
+
+
+def _bf16_module_forward(codec, name, mod, x, exact=False):
+    """The reference module on x under the CUDA autocast policy; for the two fused module names the
+    generator's own following ops (generators.py:125/141-145) are applied the same way."""
+    from _autocast_cuda import cuda_autocast_bf16
+
+    with torch.no_grad(), cuda_autocast_bf16(exact):
+        if name == "generator.conv_post":
+            return torch.tanh(codec.generator.conv_post(torch.nn.functional.silu(x)))
+        y = mod(x)
+        if name.startswith("generator.resblocks.") and name.count(".") == 2:
+            y = torch.nn.functional.silu(y)  # dcx's ParallelBlock module returns silu(mean)
+        return y
+
+
+def make_bf16(codec, audio_batch):
+    """bf16.npz: the reference's enable_bfloat16 path (`torch.autocast("cuda", bfloat16)`,
+    distil_codec.py:550,590) with CUDA's op policy applied on the CPU (`_autocast_cuda.py`):
+    * e2e on the e2e_batch clips: encoder features, x_pjt_in (bf16), codes, fp64 gaps of the
+      bf16 x_pjt_in; the bf16 decode of those codes; the reference's own spread (8 vs 1 CPU threads:
+      fp32 accumulation order) of each;
+    * per-module cases: every module's input as captured in the bf16 run (clip 0; generator modules on
+      the decode of the first GEN_FRAMES codes; encoder modules cropped to ENC_ROWS rows), its output, the reference's 8-vs-1-thread spread
+      and its distance to the same module in fp32 (how far the dtypes move the result)."""
+    from _autocast_cuda import cuda_autocast_bf16
+
+    clips = [a for a in audio_batch]
+    ng = len(clips)
+    d = {}
+    embed = codec.quantizer.grvq.rvqs[0].layers[0]._codebook.embed[0]
+    mods = _bf16_modules(codec)
+    captured = {}
+
+    def hook(name):
+        def f(_m, inp, _out):
+            if name not in captured:
+                captured[name] = inp[0].detach().clone()
+        return f
+
+    def run(threads, capture=False):
+        torch.set_num_threads(threads)
+        hs = [m.register_forward_hook(hook(n)) for n, m in mods] if capture else []
+        try:
+            with torch.no_grad():
+                mel = torch.from_numpy(np.load(os.path.join(HERE, "e2e_batch.npz"))["mel"])
+                with cuda_autocast_bf16():
+                    feat = codec.encoder(mel)
+                    ret = codec.quantizer(feat)
+                codes = ret.codes
+                if capture:  # generator modules: the decode of clip 0's first GEN_FRAMES codes
+                    with cuda_autocast_bf16():
+                        codec.generator(codec.quantizer.decode(codes[:, :1, :GEN_FRAMES]))
+                with cuda_autocast_bf16():
+                    wav = codec.generator(codec.quantizer.decode(codes))
+        finally:
+            for h_ in hs:
+                h_.remove()
+        return dict(feat=feat, x_pjt_in=ret.x_pjt_in, codes=codes, wav=wav[:, 0])
+
+    a = run(THREADS, capture=True)
+    b = run(1)
+    with torch.no_grad(), cuda_autocast_bf16():  # 1 thread, decoding the same (8-thread) codes
+        wav1 = codec.generator(codec.quantizer.decode(a["codes"]))[:, 0]
+    torch.set_num_threads(THREADS)
+    for k in ("feat", "x_pjt_in", "wav"):
+        _store(d, k, a[k])
+        d[f"spread_{k}"] = np.float64(_rel(b[k], a[k]))
+    d["spread_wav_same_codes"] = np.float64(_rel(wav1, a["wav"]))
+    d["codes"] = _np(a["codes"][0, :, :, 0]).astype(np.int64)
+    d["spread_codes_equal"] = np.float64((a["codes"] == b["codes"]).double().mean())
+    best, second, arg64 = R.top2_gap_fp64(a["x_pjt_in"].float(), embed)
+    d.update(gap_best=_np(best), gap_second=_np(second), argmin_fp64=_np(arg64).reshape(d["codes"].shape))
+    # per-module cases
+    names = []
+    for name, mod in mods:
+        x = captured[name][:1]
+        if not name.startswith("generator."):  # (B, C, T) except project_in's (B, T, C)
+            x = x[:, :ENC_ROWS] if name.endswith("project_in") else x[..., :ENC_ROWS]
+        x = x.contiguous()
+        names.append(name)
+        y = _bf16_module_forward(codec, name, mod, x)
+        torch.set_num_threads(1)
+        y1 = _bf16_module_forward(codec, name, mod, x)
+        torch.set_num_threads(THREADS)
+        ye = _bf16_module_forward(codec, name, mod, x, exact=True)
+        with torch.no_grad():
+            xf = x.float()
+            if name == "generator.conv_post":
+                yf = torch.tanh(codec.generator.conv_post(torch.nn.functional.silu(xf)))
+            else:
+                yf = mod(xf)
+                if name.startswith("generator.resblocks.") and name.count(".") == 2:
+                    yf = torch.nn.functional.silu(yf)
+        _store(d, f"m:{name}:in", x)
+        _store(d, f"m:{name}:out", y)
+        d[f"m:{name}:spread"] = np.float64(_rel(y1, y))
+        d[f"m:{name}:exact_spread"] = np.float64(_rel(ye, y))
+        d[f"m:{name}:fp32_dist"] = np.float64(_rel(yf, y))
+        print(f"  {name:40s} in {tuple(x.shape)} {str(x.dtype):15s} out {str(y.dtype):15s} exact {d[f'm:{name}:exact_spread']:.2e}"
+              f" fp32 {d[f'm:{name}:fp32_dist']:.2e}")
+    d["module_names"] = np.array(names)
+    d.update(threads=np.array(THREADS), seed=np.array(SEED), n_clips=np.array(ng))
+    np.savez_compressed(os.path.join(HERE, "bf16.npz"), **d)
+    print("bf16", {k: v.shape for k, v in d.items() if not k.startswith("m:")})
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "bf16":  # only the bf16 fixture (the others unchanged)
+        torch.manual_seed(0)
+        torch.set_num_threads(THREADS)
+        codec, _ = build_reference()
+        make_bf16(codec, np.load(os.path.join(HERE, "e2e_batch.npz"))["audio"])
+    else:
+        main()
