@@ -18,7 +18,7 @@ default c2 workload the same line carries sub-records (each skippable by a flag)
   "c4"             a C4 pass (128 ragged clips per GPU, padded to the global max), at every N;
   "c3"             (N = 1) configs[2]: encoder + GRFVQ token extraction, 256 x 10 s, bf16;
   "c5"             (N = 1) configs[4]: 1 s hops through one captured hipGraph (split-K latency mode);
-  "codes_vs_oracle" (N = 1) clip 0 of the timed C2 batch against the CPU oracle: decisive codes
+  "codes_vs_oracle" (N = 1) the first, middle and last clip of the timed C2 batch against the CPU oracle: decisive codes
                    exact, the raw code match rate and the waveform SNR (the metric's "code-index
                    bit-exact vs CPU" clause, measured on the benchmarked workload).
 
@@ -206,36 +206,45 @@ def c5_record(eng, hops: int = 100, warmup: int = 10, split_k: int = 16):
 
 
 def codes_vs_oracle(eng, runner, cfg, state):
-    """Clip 0 of the timed C2 batch (full 10 s) against the CPU oracle (oracle/reference_cpu.py, the
-    reference's algorithm on PyTorch-CPU): codes exact on every decisive frame (fp64 relative top-2
-    gap > 1e-4, computed with torch fp64 on the GPU), the raw exact-match rate, and the waveform SNR
-    (of the reference's codes decoded on the GPU when a non-decisive code differs)."""
+    """The first, middle and last clip of the timed C2 batch (full 10 s each) against the CPU oracle
+    (oracle/reference_cpu.py, the reference's algorithm on PyTorch-CPU): codes exact on every decisive
+    frame (fp64 relative top-2 gap > 1e-4, computed with torch fp64 on the GPU), the raw exact-match
+    rate, and the waveform SNR (of the reference's codes decoded on the GPU when a non-decisive code
+    differs).  Equal-length clips: each clip alone is the batch's clip (tests/test_gpu_api.py)."""
     from oracle import reference_cpu as R
 
     torch.set_num_threads(_host_threads())
-    audio = runner.audio[:1].cpu()
-    t0 = time.perf_counter()
-    ref = R.encode_decode(audio, state, cfg)
-    t_ref = time.perf_counter() - t0
-    rc = ref["codes"][0, :, :, 0].numpy()
-    gc = runner.codes[:1].cpu().numpy().astype(np.int64)
-    x = ref["x_pjt_in"].reshape(-1, ref["x_pjt_in"].shape[-1]).to(eng.device, torch.float64)
+    nb = runner.audio.shape[0]
+    clips = sorted({0, nb // 2, nb - 1})
     E = R.codebook(state["quantizer"]).to(eng.device, torch.float64)
-    d = (x ** 2).sum(1)[:, None] + (E ** 2).sum(1)[None, :] - 2.0 * x @ E.T
-    v, _ = torch.topk(d, 2, dim=1, largest=False)
-    decisive = (((v[:, 1] - v[:, 0]) / v[:, 0]) > 1e-4).cpu().numpy().reshape(rc.shape)
-    del x, E, d
-    same = np.array_equal(gc, rc)
-    wav = runner.wav[:1] if same else eng.generate(eng.vq_decode(torch.from_numpy(rc).to(torch.int32)))
-    w, r = wav.double().cpu().numpy().reshape(-1), ref["wav"][:, 0].double().numpy().reshape(-1)
-    snr = 10 * np.log10((r ** 2).sum() / max(((w - r) ** 2).sum(), 1e-300))
-    return {"clip": "clip 0 of the timed C2 batch (10 s), oracle/reference_cpu.py fp32 on the host CPU",
-            "frames": int(gc.size), "decisive_frames": int(decisive.sum()),
-            "decisive_exact": bool(np.array_equal(gc[decisive], rc[decisive])),
-            "match_rate": round(float((gc == rc).mean()), 6),
-            "waveform_snr_db": round(float(snr), 2),
-            "waveform_of": "the GPU's own codes" if same else "the reference's codes decoded on the GPU (a non-decisive code differs)",
-            "oracle_seconds": round(t_ref, 2)}
+    e2 = (E ** 2).sum(1)
+    frames = dec_frames = matches = 0
+    decisive_exact, snrs, t_ref, of = True, [], 0.0, []
+    for c in clips:
+        audio = runner.audio[c:c + 1].cpu()
+        t0 = time.perf_counter()
+        ref = R.encode_decode(audio, state, cfg)
+        t_ref += time.perf_counter() - t0
+        rc = ref["codes"][0, :, :, 0].numpy()
+        gc = runner.codes[c:c + 1].cpu().numpy().astype(np.int64)
+        x = ref["x_pjt_in"].reshape(-1, ref["x_pjt_in"].shape[-1]).to(eng.device, torch.float64)
+        d = (x ** 2).sum(1)[:, None] + e2[None, :] - 2.0 * x @ E.T
+        v, _ = torch.topk(d, 2, dim=1, largest=False)
+        decisive = (((v[:, 1] - v[:, 0]) / v[:, 0]) > 1e-4).cpu().numpy().reshape(rc.shape)
+        del x, d
+        same = np.array_equal(gc, rc)
+        wav = runner.wav[c:c + 1] if same else eng.generate(eng.vq_decode(torch.from_numpy(rc).to(torch.int32)))
+        w, r = wav.double().cpu().numpy().reshape(-1), ref["wav"][:, 0].double().numpy().reshape(-1)
+        snrs.append(round(float(10 * np.log10((r ** 2).sum() / max(((w - r) ** 2).sum(), 1e-300))), 2))
+        of.append("own codes" if same else "reference's codes")
+        frames += gc.size
+        dec_frames += int(decisive.sum())
+        matches += int((gc == rc).sum())
+        decisive_exact = decisive_exact and bool(np.array_equal(gc[decisive], rc[decisive]))
+    return {"clips": f"clips {clips} of the timed C2 batch (10 s each), oracle/reference_cpu.py fp32 on the host CPU",
+            "frames": int(frames), "decisive_frames": int(dec_frames), "decisive_exact": decisive_exact,
+            "match_rate": round(matches / frames, 6), "waveform_snr_db": snrs,
+            "waveform_of": of, "oracle_seconds": round(t_ref, 2)}
 
 
 def make_runner(eng, workload: str, rank: int, world: int, seed: int = 0):

@@ -694,11 +694,31 @@ int run_conv_split(dcx_codec* h, const ConvW& w, const ConvCall& c, const ConvPa
   return DCX_OK;
 }
 
+#ifdef DCX_DIAG_DUP
+// Diagnostic builds: with DCX_DIAG_DUP=1 (no stores) or 2 (no epilogue) every conv launch is preceded
+// by a timing copy on the same (real) inputs that writes nothing, profiled as "diag:<kernel>", so
+// kernel tables compare each launch with and without its epilogue's stores on identical data.
+int diag_dup_mode() {
+  const char* e = std::getenv("DCX_DIAG_DUP");
+  return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
+}
+#endif
+
 int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, bool force_f32 = false) {
   ConvParams p;
   RUN(conv_params(h, w, c, force_f32, p));
   const int S = force_f32 ? 1 : split_factor(h, w, c, p);
   if (S > 1) return run_conv_split(h, w, c, p, S, s);
+#ifdef DCX_DIAG_DUP
+  if (const int dm = diag_dup_mode()) {
+    ConvParams q = p;
+    q.diag_skip = dm;
+    ProfScope pd(h, s);
+    const char* kn = "conv";
+    HIPCHK(h, dcx::launch_conv(q, c.batch, w.phases, s, &kn));
+    pd.done((std::string("diag:") + kn).c_str(), conv_flops(w, c), conv_bytes(w, c));
+  }
+#endif
   ProfScope ps(h, s);
   const char* kname = "conv";
   HIPCHK(h, dcx::launch_conv(p, c.batch, w.phases, s, &kname));
@@ -719,6 +739,19 @@ int run_conv_group(dcx_codec* h, const ConvW* const* w, const ConvCall* c, int n
     same = same && c[i].batch == c[0].batch && w[i]->phases == 1;
   }
   if (same && n > 1) {
+#ifdef DCX_DIAG_DUP
+    if (const int dm = diag_dup_mode()) {
+      ConvParams q[dcx::kMaxGroup];
+      for (int i = 0; i < n; ++i) {
+        q[i] = p[i];
+        q[i].diag_skip = dm;
+      }
+      ProfScope pd(h, s);
+      const char* kn = "conv_group";
+      const hipError_t e = dcx::launch_conv_group(q, n, c[0].batch, s, &kn);
+      if (e == hipSuccess) pd.done((std::string("diag:") + kn).c_str(), fl, by);
+    }
+#endif
     ProfScope ps(h, s);
     const char* kname = "conv_group";
     const hipError_t e = dcx::launch_conv_group(p, n, c[0].batch, s, &kname);
@@ -1735,21 +1768,30 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
     }
     // The bf16 mode's table: project_out under the reference's autocast (residual_vq.py:138 inside
     // distil_codec.py:590), bf16(bf16(E) W_out16^T + b_out16) by the one-product conv on the codebook
-    // planes; row NC = bf16(b_out) (the masked code).  Built in a scratch fp32 table, then split.
+    // as activation planes (scratch); row NC = bf16(b_out) (the masked code).  Built in a scratch fp32
+    // table, then split.
     h->ptable6b = (unsigned short*)B.alloc((size_t)(NC + 1) * D * 3 / 2);
-    if (!B.bad() && !B.dry && h->codebook6) {
+    if (!B.bad() && !B.dry && h->codebook) {
       float* tmp = nullptr;
+      unsigned short* e6 = nullptr;
       if (hipMalloc(&tmp, sizeof(float) * (size_t)(NC + 1) * D) != hipSuccess) return fail(h, DCX_ERR_OOM, "hipMalloc failed");
+      if (hipMalloc(&e6, sizeof(unsigned short) * 3 * (size_t)NC * CD) != hipSuccess) {
+        hipFree(tmp);
+        return fail(h, DCX_ERR_OOM, "hipMalloc failed");
+      }
+      int rc = dcx::launch_split_planes(h->codebook, e6, NC, CD, 0, 0) == hipSuccess
+                   ? DCX_OK : fail(h, DCX_ERR_HIP, "codebook split failed");
       const int mode = h->gemm_mode;
       h->gemm_mode = DCX_GEMM_BF16;
-      ConvCall cp = pointwise(CAct(h->codebook, h->codebook6), NC);
+      ConvCall cp = pointwise(CAct(h->codebook, e6), NC);
       cp.y = tmp;
-      int rc = run_conv(h, pout, cp, 0);
+      if (rc == DCX_OK) rc = run_conv(h, pout, cp, 0);
       h->gemm_mode = mode;
       if (rc == DCX_OK &&
           (hipMemcpy(tmp + (size_t)NC * D, pout.b16, sizeof(float) * D, hipMemcpyDeviceToDevice) != hipSuccess ||
            dcx::launch_split_planes(tmp, h->ptable6b, NC + 1, D, 0, 0) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
         rc = fail(h, DCX_ERR_HIP, "bf16 decode-table build failed");
+      hipFree(e6);
       hipFree(tmp);
       if (rc != DCX_OK) return rc;
     }

@@ -72,6 +72,9 @@ struct ConvParams {
   // whole number of kunit chunks; batch = clips * ksplit, and slice s of clip c is output clip
   // s * clips + c (partial sums, plain fp32: launch_splitk_epilogue finishes them)
   int ksplit, kunit;
+  // diagnostic builds (-DDCX_DIAG_DUP) only: 1 = compute the epilogue but store nothing, 2 = no
+  // epilogue at all (a timing copy launched before the real launch, on the real inputs)
+  int diag_skip;
 };
 
 // Independent convs issued as one launch (launch_conv_group); problem k owns logical tiles

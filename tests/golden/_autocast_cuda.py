@@ -73,14 +73,22 @@ class CudaAutocastPolicy(TorchFunctionMode):
 
     exact=True: the lower-precision ops take the same bf16 operands but accumulate in fp64 and round
     once to bf16 (an idealised kernel).  Its distance to the fp32-accumulating CPU kernels measures how
-    much a module's bf16 output moves with accumulation order alone (the tests' noise scale)."""
+    much a module's bf16 output moves with accumulation order alone (the tests' noise scale).
+    wn64=True: weight-normed convs fold torch._weight_norm(v, g) in fp64 and round the result to fp32,
+    as the library does once at load, instead of the reference's fp32 fold.  In bf16
+    the two folds round a few weights to different bf16 values (where the fp32 folds straddle a bf16
+    rounding boundary), which moves a chained module's output by more than accumulation order does."""
 
-    def __init__(self, exact: bool = False):
+    def __init__(self, exact: bool = False, wn64: bool = False):
         super().__init__()
         self.exact = exact
+        self.wn64 = wn64
 
     def __torch_function__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
+        if self.wn64 and _name(func) == "_weight_norm":  # torch._weight_norm(v, g, dim) folded in fp64
+            v, g = args[0], args[1]
+            return func(v.double(), g.double(), *args[2:], **kwargs).to(v.dtype)
         if torch.is_autocast_enabled("cuda"):
             n = _name(func)
             if n in _LOWER and self.exact:
@@ -99,13 +107,14 @@ class CudaAutocastPolicy(TorchFunctionMode):
 
 
 @contextlib.contextmanager
-def cuda_autocast_bf16(exact: bool = False):
+def cuda_autocast_bf16(exact: bool = False, wn64: bool = False):
     """`with torch.autocast("cuda", torch.bfloat16)` as the reference's GPU run sees it, on CPU tensors
-    (exact: fp64 accumulation inside the bf16 ops, see CudaAutocastPolicy)."""
+    (exact: fp64 accumulation inside the bf16 ops; wn64: weight norm folded in fp64; see
+    CudaAutocastPolicy)."""
     prev = torch.is_autocast_enabled("cuda")
     torch.set_autocast_enabled("cuda", True)
     try:
-        with CudaAutocastPolicy(exact):
+        with CudaAutocastPolicy(exact, wn64):
             yield
     finally:
         torch.set_autocast_enabled("cuda", prev)

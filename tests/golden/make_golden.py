@@ -221,12 +221,12 @@ def _bf16_modules(codec):
     return mods
 
 
-def _bf16_module_forward(codec, name, mod, x, exact=False):
+def _bf16_module_forward(codec, name, mod, x, exact=False, wn64=False):
     """The reference module on x under the CUDA autocast policy; for the two fused module names the
     generator's own following ops (generators.py:125/141-145) are applied the same way."""
     from _autocast_cuda import cuda_autocast_bf16
 
-    with torch.no_grad(), cuda_autocast_bf16(exact):
+    with torch.no_grad(), cuda_autocast_bf16(exact, wn64):
         if name == "generator.conv_post":
             return torch.tanh(codec.generator.conv_post(torch.nn.functional.silu(x)))
         y = mod(x)
@@ -284,8 +284,13 @@ def make_bf16(codec, audio_batch):
     with torch.no_grad(), cuda_autocast_bf16():  # 1 thread, decoding the same (8-thread) codes
         wav1 = codec.generator(codec.quantizer.decode(a["codes"]))[:, 0]
     torch.set_num_threads(THREADS)
+    with torch.no_grad(), cuda_autocast_bf16(wn64=True):  # the weight norm folded in fp64 (as the library)
+        wav_wn = codec.generator(codec.quantizer.decode(a["codes"]))[:, 0]
+    _store(d, "wav_wn64", wav_wn)
+    d["wn64_dist_wav"] = np.float64(_rel(wav_wn, a["wav"]))
     for k in ("feat", "x_pjt_in", "wav"):
-        _store(d, k, a[k])
+        if k != "wav":  # the decode is stored with the fp64 weight-norm fold (wav_wn64)
+            _store(d, k, a[k])
         d[f"spread_{k}"] = np.float64(_rel(b[k], a[k]))
     d["spread_wav_same_codes"] = np.float64(_rel(wav1, a["wav"]))
     d["codes"] = _np(a["codes"][0, :, :, 0]).astype(np.int64)
@@ -305,6 +310,7 @@ def make_bf16(codec, audio_batch):
         y1 = _bf16_module_forward(codec, name, mod, x)
         torch.set_num_threads(THREADS)
         ye = _bf16_module_forward(codec, name, mod, x, exact=True)
+        yw = _bf16_module_forward(codec, name, mod, x, wn64=True) if name.startswith("generator.") else y
         with torch.no_grad():
             xf = x.float()
             if name == "generator.conv_post":
@@ -314,7 +320,11 @@ def make_bf16(codec, audio_batch):
                 if name.startswith("generator.resblocks.") and name.count(".") == 2:
                     yf = torch.nn.functional.silu(yf)
         _store(d, f"m:{name}:in", x)
-        _store(d, f"m:{name}:out", y)
+        if name.startswith("generator."):  # weight-normed convs: the output with the library's fp64 fold
+            _store(d, f"m:{name}:out_wn64", yw)
+            d[f"m:{name}:wn64_dist"] = np.float64(_rel(yw, y))
+        else:
+            _store(d, f"m:{name}:out", y)
         d[f"m:{name}:spread"] = np.float64(_rel(y1, y))
         d[f"m:{name}:exact_spread"] = np.float64(_rel(ye, y))
         d[f"m:{name}:fp32_dist"] = np.float64(_rel(yf, y))
