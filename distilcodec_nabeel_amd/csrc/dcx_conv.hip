@@ -340,7 +340,9 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
         if (p.round_bf16) x[h] = round_bf16x4(x[h]);
         switch (p.epi) {
           case EPI_GELU:
-            if (p.round_bf16) {
+            // planes modes (x6, bf16): the branch-free GELU (abs error 4.5e-7 against fp64, below
+            // torch's fp32 erff GELU's 1.2e-6); the IEEE fp32 mode keeps erff
+            if (p.w6) {
 #ifndef DCX_EPI_NOGELU  // timing build: the bf16 GELU left out
 #pragma unroll
               for (int e = 0; e < 4; e += 2) {
@@ -350,7 +352,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
               }
 #endif
               // a compact-only output rounds to bf16 in its store (the same RNE bits)
-              if (p.y || y6s || p.y2 || p.y_compact != 1) x[h] = round_bf16x4(x[h]);
+              if (p.round_bf16 && (p.y || y6s || p.y2 || p.y_compact != 1)) x[h] = round_bf16x4(x[h]);
             } else {
 #pragma unroll
               for (int e = 0; e < 4; ++e) x[h][e] = gelu_f(x[h][e]);
@@ -470,7 +472,7 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(const ConvParams p
   switch (p.epi) {
     case EPI_GELU:
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] = p.round_bf16 ? gelu_bf16_f(x[e]) : gelu_f(x[e]);
+      for (int e = 0; e < 4; ++e) x[e] = p.w6 ? gelu_bf16_f(x[e]) : gelu_f(x[e]);
       if (p.round_bf16) x = round_bf16x4(x);
       break;
     case EPI_GAMMA_RES:
@@ -3155,6 +3157,14 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_bq(const ConvParams p) {
   epilogue_top2_q<BM, BN, 4, WN>(p, acc, q0, co0, nt, ntiles, reinterpret_cast<float*>(lds));
 }
 
+// 64-byte LDS rows of vq_prefilter_b1: the 16-byte piece q of row r sits in slot q ^ b1_swz(r), with
+// b1_swz(r) = (0, 2, 3, 1)[(r >> 2) & 3].  A ds_read_b128 is serviced in four 16-lane groups,
+// {0-3, 12-15, 20-27}, {4-11, 16-19, 28-31} and the same + 32 (MI355X_MICROARCH.md §LDS), and lane l
+// reads piece l >> 4 of row l & 15: this map gives the 16 lanes of every group 16 distinct bank quads.
+// (Round 3's (r >> 2) & 3 paired up two lanes per quad in every group: 2-way conflicts, 46 % of the
+// kernel's LDS cycles in PMC, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE.)
+__device__ __forceinline__ int b1_swz(int r) { return (0x1320 >> (((r >> 2) & 3) * 4)) & 3; }
+
 // ---------------------------------------------------------------------------------------------
 // vq_prefilter_b1: one bf16 product per term, x_h . e_h', in both arithmetic modes (round 3).
 //
@@ -3171,8 +3181,7 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_bq(const ConvParams p) {
 // 16-byte pieces of 8 channels).  Both operands arrive as 64-byte runs per row / code and step:
 // x_pjt_in compact ([rows][CD] bf16, the project_in epilogue's y_compact == 1 output) and the
 // codebook as launch_repack_codebook_b1 packs it ([CD/32][NC][32] bf16).  LDS images: 64-byte
-// rows, piece q in slot q ^ ((row >> 2) & 3) (vq_prefilter_bk's x image), conflict-free for the
-// four lane groups of a ds_read_b128.  Ring: NS slots of 16 + 16 KiB on the ping-pong schedule
+// rows, piece q in slot q ^ b1_swz(row), conflict-free for the four lane groups of a ds_read_b128.  Ring: NS slots of 16 + 16 KiB on the ping-pong schedule
 // of vq_prefilter_bk generalised to NS slots: step t is issued by group 0 in MEM0(t - NS) and by
 // group 1 in MEM1(t - NS + 1), and each wave retires its pieces NS - 2 memory segments later.
 // ---------------------------------------------------------------------------------------------
@@ -3210,13 +3219,13 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_b1(const ConvParams p) {
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     const int u = (group * A_G + i * 4 + gw) * 64 + lane;
-    const int row = u >> 2, pc = (u & 3) ^ ((row >> 2) & 3);
+    const int row = u >> 2, pc = (u & 3) ^ b1_swz(row);
     a_off[i] = row * arow + pc * 16;
   }
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
     const int u = (group * B_G + i * 4 + gw) * 64 + lane;
-    const int code = u >> 2, pc = (u & 3) ^ ((code >> 2) & 3);
+    const int code = u >> 2, pc = (u & 3) ^ b1_swz(code);
     b_off[i] = (co0 + code) * 64 + pc * 16;
   }
   unsigned short* const a_dst = lds + (group * A_G + gw) * 512;
@@ -3237,12 +3246,12 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_b1(const ConvParams p) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int r = wm * WR + i * 16 + l16;
-      af[i] = *reinterpret_cast<const s16x8*>(A + r * RW + ((pq ^ ((r >> 2) & 3)) << 3));
+      af[i] = *reinterpret_cast<const s16x8*>(A + r * RW + ((pq ^ b1_swz(r)) << 3));
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = wn * WC + j * 16 + l16;
-      bfr[j] = *reinterpret_cast<const s16x8*>(Bs + col * RW + ((pq ^ ((col >> 2) & 3)) << 3));
+      bfr[j] = *reinterpret_cast<const s16x8*>(Bs + col * RW + ((pq ^ b1_swz(col)) << 3));
     }
   };
   f32x4 acc[TM][TN];

@@ -103,6 +103,9 @@ struct ResPairParams {
   float* mean_out;
   long long bstride;  // elements between clips
   int L, batch, C;
+  // conv_res_pair_g: a workgroup barrier after every tap_sync-th tap of a conv (0: none), which
+  // bounds how far the two waves of a SIMD drift apart before the image hand-offs
+  int tap_sync;
 };
 
 // Launchers (all stream-ordered, no allocation).  Return hipError_t of the launch.

@@ -29,6 +29,7 @@
 // plane), so every ds_read_b128 of 16 consecutive rows of one piece is conflict-free at any tap
 // offset, and the weight slot is the global tap slice [chunk][Cout][96 B] copied as is.
 #include <algorithm>
+#include <cstdlib>
 
 #include "dcx_kernels.h"
 #include "dcx_planes.h"
@@ -553,7 +554,11 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_g(const ResPairParams p)
       // ---- c1 over rows [r0 - 8, r0 + R + 8) from the S image
 #pragma unroll
       for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int j = 0; j < k; ++j) tap(acc, G::H1 + (j - hk) * d, RB, next_tap(m, 0, j), no_hook);
+      const int ts = p.tap_sync;
+      for (int j = 0; j < k; ++j) {
+        tap(acc, G::H1 + (j - hk) * d, RB, next_tap(m, 0, j), no_hook);
+        if (ts && (j + 1) % ts == 0 && j + 1 < k) rp_barrier();  // workgroup-uniform
+      }
       RP_T(tb);
       rp_barrier();  // every wave's S reads are done before T overwrites them
       // ---- T image: silu(c1 + b1) planes over the S image (zero outside the clip)
@@ -615,9 +620,15 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_g(const ResPairParams p)
         for (int kk = NIT / 2; kk < NIT; ++kk) issue_fill_item(nsrc, nsr0, kk);
       };
       tap(acc, 8 - hk, nrb2, next_tap(m, 1, 0), res_hook);
+      if (ts == 1) rp_barrier();
       tap(acc, 9 - hk, nrb2, next_tap(m, 1, 1), pf_hook0);
+      if (ts && 2 % ts == 0) rp_barrier();
       tap(acc, 10 - hk, nrb2, next_tap(m, 1, 2), pf_hook1);
-      for (int j = 3; j < k; ++j) tap(acc, 8 + j - hk, nrb2, next_tap(m, 1, j), no_hook);
+      if (ts && 3 % ts == 0 && 3 < k) rp_barrier();
+      for (int j = 3; j < k; ++j) {
+        tap(acc, 8 + j - hk, nrb2, next_tap(m, 1, j), no_hook);
+        if (ts && (j + 1) % ts == 0 && j + 1 < k) rp_barrier();
+      }
       RP_T(te);
       // ---- epilogue: state + c2 + b2 (rows past the clip end are dropped)
 #pragma unroll
@@ -705,10 +716,22 @@ hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** k
   // DCX_RP_OLD=1 (read at each launch; A/B and tests) runs the step schedule at C = 32 too.
   const char* oe = getenv("DCX_RP_OLD");
   const bool old = oe && *oe && *oe != '0';
+  // A/B switches (read at each launch): DCX_RP_G64=1 runs the barrier-free kernel at C = 64 too,
+  // DCX_RP_SYNC=n puts a barrier after every n-th tap of its conv loops
+  const char* g64 = getenv("DCX_RP_G64");
+  const char* sy = getenv("DCX_RP_SYNC");
+  ResPairParams q = p;
+  q.tap_sync = sy && *sy ? std::max(0, std::atoi(sy)) : 0;
   if (p.C == 32 && !old) {
     if (kname) *kname = p.mean_out ? "conv_res_pair_g<32,mean>" : "conv_res_pair_g<32>";
-    if (p.mean_out) hipLaunchKernelGGL((conv_res_pair_g<32, true>), dim3(grid), dim3(512), 0, s, p);
-    else hipLaunchKernelGGL((conv_res_pair_g<32, false>), dim3(grid), dim3(512), 0, s, p);
+    if (p.mean_out) hipLaunchKernelGGL((conv_res_pair_g<32, true>), dim3(grid), dim3(512), 0, s, q);
+    else hipLaunchKernelGGL((conv_res_pair_g<32, false>), dim3(grid), dim3(512), 0, s, q);
+    return hipGetLastError();
+  }
+  if (p.C == 64 && !old && g64 && *g64 == '1') {
+    if (kname) *kname = p.mean_out ? "conv_res_pair_g<64,mean>" : "conv_res_pair_g<64>";
+    if (p.mean_out) hipLaunchKernelGGL((conv_res_pair_g<64, true>), dim3(grid), dim3(512), 0, s, q);
+    else hipLaunchKernelGGL((conv_res_pair_g<64, false>), dim3(grid), dim3(512), 0, s, q);
     return hipGetLastError();
   }
   if (p.C == 32) {

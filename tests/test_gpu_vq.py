@@ -27,7 +27,12 @@ def _argmin_fp64(P: torch.Tensor, E: torch.Tensor, chunk: int = 1024) -> np.ndar
     for s in range(0, P.shape[0], chunk):
         x = P[s: s + chunk].to("cuda:0", torch.float64)
         d = (x ** 2).sum(1)[:, None] + e2[None, :] - 2.0 * (x @ E64.T)
-        out.append(torch.argmin(d, dim=1).cpu())  # first index of the minimum
+        # first index of the minimum, exact ties included: the fp64 GEMM may round identical codebook
+        # rows differently in different column tiles, so distances within 1e-12 relative of the
+        # minimum (far below any fp32-valued gap) count as ties
+        m = d.min(dim=1, keepdim=True).values
+        tie = d <= m + 1e-12 * m.abs()
+        out.append(torch.argmax(tie.to(torch.int8), dim=1).cpu())
     return torch.cat(out).numpy()
 
 
