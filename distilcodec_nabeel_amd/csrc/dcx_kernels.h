@@ -75,6 +75,10 @@ struct ConvParams {
   // diagnostic builds (-DDCX_DIAG_DUP) only: 1 = compute the epilogue but store nothing, 2 = no
   // epilogue at all (a timing copy launched before the real launch, on the real inputs)
   int diag_skip;
+  // conv_gemm_bf16dp with GELU: > 0 = GELU from its LDS table of the bf16 GELU (same bits), a wave
+  // with a table offset >= gelu_lut storing the evaluated epilogue instead; 0 = evaluated (set by
+  // launch_conv; DCX_GELU_LUT)
+  int gelu_lut;
 };
 
 // Independent convs issued as one launch (launch_conv_group); problem k owns logical tiles

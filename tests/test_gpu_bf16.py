@@ -181,3 +181,35 @@ def test_register_epilogue_same_bits(beng):
         outs.append((feat.clone(), codes.clone(), pin.clone(), q.clone()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_persistent_same_bits(beng):
+    """conv_gemm_bf16dp (the pwconv1 launches as one persistent step stream, GELU from the LDS table)
+    against conv_gemm_bf16dm<true> (DCX_BF16_PERSIST=0): encoder features, x_pjt_in and codes bit for
+    bit, with the table (default), with table limits that send waves with a pre-GELU |x| >= 4
+    (DCX_GELU_LUT=8448, a few) or >= 1 (7936, nearly all) through the evaluated epilogue over the
+    table's stores, and evaluated throughout (DCX_GELU_LUT=0).  4 x 11 s clips, every 1x1 conv on the bf16 kernels."""
+    import os
+
+    from distilcodec_nabeel_amd import synth
+
+    n = 24000 * 11
+    audio = torch.zeros(4, n + 1)
+    for i, c in enumerate(synth.clips(4, n, seed=13, kind="mix")):
+        audio[i, 1:] = torch.from_numpy(c)
+    audio = audio.cuda()
+    outs = []
+    for env in ({"DCX_BF16_PERSIST": "0"}, {}, {"DCX_GELU_LUT": "8448"}, {"DCX_GELU_LUT": "7936"},
+                {"DCX_GELU_LUT": "0"}):
+        os.environ.update(env)
+        try:
+            feat = beng.encode(beng.mel(audio))
+            codes, pin, _, q = beng.vq_encode(feat, want_fup=False)
+            torch.cuda.synchronize()
+        finally:
+            for k in env:
+                del os.environ[k]
+        outs.append((feat.clone(), codes.clone(), pin.clone(), q.clone()))
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
