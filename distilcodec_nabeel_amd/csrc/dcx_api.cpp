@@ -726,6 +726,80 @@ int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, boo
   return DCX_OK;
 }
 
+// Split-K latency mode, grouped (round 4): the few-tile convs of one ResBlock dilation index (all
+// three split-eligible) as ONE conv launch whose members get K-slice counts in proportion to their
+// K (taps x chunks), within the CU count of workgroups, and ONE launch of their reduces, instead of
+// two launches per conv (a C5 hop spent ~7 us per reduce launch, 107 of them).  Returns 1 when the
+// group does not qualify (the caller splits the members one by one).
+int run_conv_group_split(dcx_codec* h, const ConvW* const* w, const ConvCall* c, ConvParams* p, int n, double fl,
+                         double by, hipStream_t s) {
+  if (n < 2 || std::getenv("DCX_SPLIT_GROUP_OFF")) return 1;
+  long long tiles[dcx::kMaxGroup], out[dcx::kMaxGroup], chunks[dcx::kMaxGroup];
+  int S[dcx::kMaxGroup], smax[dcx::kMaxGroup];
+  long long total = 0;
+  for (int i = 0; i < n; ++i) {
+    if (split_factor(h, *w[i], c[i], p[i]) < 2 || w[i]->taps < 3 || w[i]->out_mul != 1) return 1;
+    tiles[i] = (long long)c[i].batch * ((c[i].Lq + 255) / 256) * (w[i]->cout / 128);
+    out[i] = (long long)c[i].batch * p[i].y_bstride;
+    const int unit = w[i]->taps % 2 ? 2 : 1;
+    chunks[i] = (long long)w[i]->taps * (w[i]->cin / 16);
+    smax[i] = (int)std::min<long long>(kSplitMax, (w[i]->cin / 16) / unit);
+    S[i] = 1;
+    total += tiles[i];
+  }
+  // K slices: repeatedly give one more slice to the member whose slices are longest, while the
+  // grid stays within one workgroup per CU
+  for (;;) {
+    int best = -1;
+    for (int i = 0; i < n; ++i)
+      if (S[i] < smax[i] && total + tiles[i] <= 256 &&
+          (best < 0 || chunks[i] * S[best] > chunks[best] * S[i]))
+        best = i;
+    if (best < 0) break;
+    ++S[best];
+    total += tiles[best];
+  }
+  long long need = 0;
+  for (int i = 0; i < n; ++i) need += S[i] > 1 ? S[i] * out[i] : 0;
+  if (need > kSplitMax * kSplitMaxOut) return 1;
+  ProfScope ps(h, s);
+  ConvParams q[dcx::kMaxGroup], r[dcx::kMaxGroup];
+  const float* part[dcx::kMaxGroup];
+  int rs[dcx::kMaxGroup];
+  long long rstride[dcx::kMaxGroup];
+  int nr = 0;
+  long long off = 0;
+  for (int i = 0; i < n; ++i) {
+    q[i] = p[i];
+    q[i].ksplit = S[i];
+    if (S[i] > 1) {  // partial sums into the split buffer, the epilogue in the reduce
+      q[i].kunit = w[i]->taps % 2 ? 2 : 1;
+      q[i].bias = q[i].gamma = q[i].res = nullptr;
+      q[i].macc = nullptr;
+      q[i].y = h->split_buf + off;
+      q[i].y2 = nullptr;
+      q[i].y6 = q[i].y6s = nullptr;
+      q[i].epi = dcx::EPI_BIAS;
+      q[i].mean_mode = dcx::MEAN_NONE;
+      q[i].y_compact = 0;
+      q[i].round_bf16 = 0;
+      r[nr] = p[i];
+      part[nr] = h->split_buf + off;
+      rs[nr] = S[i];
+      rstride[nr] = out[i];
+      ++nr;
+      off += S[i] * out[i];
+    }
+  }
+  const char* kname = "conv_group";
+  const hipError_t e = dcx::launch_conv_split_group(q, n, c[0].batch, s, &kname);
+  if (e == hipErrorNotSupported) return 1;
+  HIPCHK(h, e);
+  if (nr) HIPCHK(h, dcx::launch_splitk_epilogue_group(r, part, rs, rstride, nr, c[0].batch, s));
+  ps.done((std::string("splitk:") + kname).c_str(), fl, by);
+  return DCX_OK;
+}
+
 // n independent convs (same batch) as one grouped launch when the kernel family allows it
 // (dcx::launch_conv_group), otherwise one by one; the results are the same bits either way.
 int run_conv_group(dcx_codec* h, const ConvW* const* w, const ConvCall* c, int n, hipStream_t s) {
@@ -737,6 +811,10 @@ int run_conv_group(dcx_codec* h, const ConvW* const* w, const ConvCall* c, int n
     fl += conv_flops(*w[i], c[i]);
     by += conv_bytes(*w[i], c[i]);
     same = same && c[i].batch == c[0].batch && w[i]->phases == 1;
+  }
+  if (same && n > 1 && h->split_k >= 2) {
+    const int rc = run_conv_group_split(h, w, c, p, n, fl, by, s);
+    if (rc != 1) return rc;
   }
   if (same && n > 1) {
 #ifdef DCX_DIAG_DUP

@@ -491,10 +491,8 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
 // Split-K reduce: v = bias + sum of the K-slices' partial sums (in slice order), then the epilogue
 // of epilogue_lds element by element (one thread per 4 output channels of a row).
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) splitk_epilogue_kernel(const ConvParams p, const float* __restrict__ part,
-                                                              int splits, long long stride, long long total4) {
-  const long long i4 = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i4 >= total4) return;
+__device__ __forceinline__ void splitk_epi4(const ConvParams& p, const float* __restrict__ part, int splits,
+                                            long long stride, long long i4) {
   const int c4n = p.Cout / 4;
   const long long rowi = i4 / c4n;  // (phase, clip, q)
   const int co = (int)(i4 - rowi * c4n) * 4;
@@ -548,6 +546,23 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(const ConvParams p
     if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
     if (p.y6s) store_planes4(p.y6s + ob * 3, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
   }
+}
+
+__global__ void __launch_bounds__(256) splitk_epilogue_kernel(const ConvParams p, const float* __restrict__ part,
+                                                              int splits, long long stride, long long total4) {
+  const long long i4 = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i4 < total4) splitk_epi4(p, part, splits, stride, i4);
+}
+
+// the reduces of a grouped split-K launch in one grid (member k: blocks [start[k], start[k + 1]))
+__global__ void __launch_bounds__(256) splitk_epilogue_group_kernel(const SplitEpiGroup g) {
+  const int t = blockIdx.x;
+  const int k = t >= g.start[1] ? (t >= g.start[2] ? 2 : 1) : 0;
+  const long long i4 = (long long)(t - g.start[k]) * 256 + threadIdx.x;
+  if (i4 >= g.total4[k]) return;
+  if (k == 0) splitk_epi4(g.p[0], g.part[0], g.splits[0], g.stride[0], i4);
+  else if (k == 1) splitk_epi4(g.p[1], g.part[1], g.splits[1], g.stride[1], i4);
+  else splitk_epi4(g.p[2], g.part[2], g.splits[2], g.stride[2], i4);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1149,7 +1164,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) conv_gemm_x6w8(const ConvPara
 // waves with the same 64 x 64 wave tiles, so the staging VALU of one group overlaps the other
 // group's MFMAs.
 template <int HALO, int BN, bool AF32 = false>
-__global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
+__device__ __forceinline__ void x6pp_tile(const ConvParams& p, const int wg, const int b, const int ph) {
   // wave tiles 64 x (BN / 2): 24 MFMAs per segment at BN = 128
   static_assert(BN == 128 || BN == 256 || (AF32 && BN == 64), "column tile");
   constexpr int BM = AF32 ? 512 : 256, WN = AF32 ? 1 : 2, WM = 8 / WN;
@@ -1168,8 +1183,6 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
   const int group = __builtin_amdgcn_readfirstlane(tid >> 8), gt = tid & 255;
   const int wm = wave / WN, wn = wave % WN;
   const int ntiles = p.Cout / BN;
-  int wg, b, ph;
-  flat_tile(((p.Lq + BM - 1) / BM) * ntiles, p.batch, wg, b, ph);
   const int mt = wg / ntiles, nt = wg - mt * ntiles;
   const int q0 = mt * BM, co0 = nt * BN;
   int clip, c0, nchunks;
@@ -1678,6 +1691,30 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6lm(const ConvParams p) {
   }
 #endif
   epilogue_lds<BM, BN, 4, WN, (2 * ABUF + 2 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+}
+
+template <int HALO, int BN, bool AF32 = false>
+__global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
+  constexpr int BM = AF32 ? 512 : 256;
+  int wg, b, ph;
+  flat_tile(((p.Lq + BM - 1) / BM) * (p.Cout / BN), p.batch, wg, b, ph);
+  x6pp_tile<HALO, BN, AF32>(p, wg, b, ph);
+}
+
+// Grouped split-K launch (round 4, the split-K latency mode): up to 3 independent halo convs (the
+// three ResBlocks' convs of one dilation index) in one grid, member k with its own K-slice count
+// (ConvParams::ksplit; its clips are virtual: slice * clips + clip).  Member by raw block index, the
+// XCD remap inside the member, as conv_gemm_x6dq_group.
+__global__ void __launch_bounds__(512, 2) conv_gemm_x6pp_group(const ConvGroup g) {
+  const int t = blockIdx.x;
+  const int k = t >= g.start[1] ? (t >= g.start[2] ? 2 : 1) : 0;
+  const int local = xcd_remap(t - g.start[k], g.start[k + 1] - g.start[k]);
+  const int b = local / g.tiles_per_clip[k];
+  ConvParams p;  // a private copy (see conv_gemm_x6dq_group)
+  if (k == 0) p = g.p[0];
+  else if (k == 1) p = g.p[1];
+  else p = g.p[2];
+  x6pp_tile<64, 128>(p, local - b * g.tiles_per_clip[k], b, 0);
 }
 
 template <int HALO>
@@ -3481,8 +3518,13 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_b1(const ConvParams p) {
   const int q0 = mt * BM, co0 = nt * BN;
   const int nsteps = p.Cin / 32;
   const int arow = p.ldx * 2;  // bytes per compact row
+#ifdef DCX_VQ_DIAG_L2  // timing build: every tile loads row panel 0 and code tile 0 (L2-resident operands)
+  const int lq0 = 0, lco0 = 0;
+#else
+  const int lq0 = q0, lco0 = co0;
+#endif
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.x6 + (long long)q0 * p.ldx), 0, min(BM, p.Lq - q0) * arow, 0x00020000);
+      (void*)(p.x6 + (long long)lq0 * p.ldx), 0, min(BM, p.Lq - lq0) * arow, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wc, 0, nsteps * p.Cout * 64, 0x00020000);
 
   int a_off[A_PW], b_off[B_PW];
@@ -3496,7 +3538,7 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_b1(const ConvParams p) {
   for (int i = 0; i < B_PW; ++i) {
     const int u = (group * B_G + i * 4 + gw) * 64 + lane;
     const int code = u >> 2, pc = (u & 3) ^ b1_swz(code);
-    b_off[i] = (co0 + code) * 64 + pc * 16;
+    b_off[i] = (lco0 + code) * 64 + pc * 16;
   }
   unsigned short* const a_dst = lds + (group * A_G + gw) * 512;
   unsigned short* const b_dst = lds + NS * ABUF + (group * B_G + gw) * 512;
@@ -3530,14 +3572,23 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_b1(const ConvParams p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto mfma = [&]() {
+#ifdef DCX_VQ_STATICPRIO  // A/B: group 1 at priority 1 throughout, no per-segment flips (MI355X_MICROARCH.md
+                          // "Two waves per SIMD" item 4); the MFMA cluster fenced for the scheduler instead
+    __builtin_amdgcn_sched_barrier(0);
+#else
     __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
                                                             __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
+#ifdef DCX_VQ_STATICPRIO
+    __builtin_amdgcn_sched_barrier(0);
+#else
     __builtin_amdgcn_s_setprio(0);
+#endif
   };
   auto inc = [](int& slot) { slot = slot == NS - 1 ? 0 : slot + 1; };
   // pieces this wave may leave in flight at the end of a memory segment: its shares of the steps
@@ -3547,34 +3598,65 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_b1(const ConvParams p) {
   for (int t = 0; t < NS && t < nsteps; ++t) dma_step(t, t);
   // group 0 reads step 0 now and step 1 in segment 1 (its own MFMA segment 0 comes first)
   wait_dma(group == 0 ? in_flight(2, NS - 1) : in_flight(1, NS - 1));
+#ifdef DCX_VQ_STATICPRIO
+  if (group == 1) __builtin_amdgcn_s_setprio(1);
+#endif
   seg_barrier();
+#ifdef DCX_SEG_DIAG
+  unsigned long long sd[5] = {};  // per step: mfma issue, barrier, reads + DMA issue, DMA wait, barrier
+#endif
   if (group == 0) {
     readF(0);
     int rs = 1, ws = 0;
     for (int s = 0; s < nsteps; ++s) {
+      DCX_SEGT(ta);
       mfma();  // MFMA(s)
+      DCX_SEGT(tb);
       seg_barrier();
+      DCX_SEGT(tc);
       if (s + 1 < nsteps) readF(rs);  // MEM0(s): fragments of step s + 1, issue step s + NS
       if (s + NS < nsteps) dma_step(s + NS, ws);
+      DCX_SEGT(td);
       wait_dma(in_flight(s + 3, s + NS));
+      DCX_SEGT(te);
       seg_barrier();
+      DCX_SEGT(tf);
+#ifdef DCX_SEG_DIAG
+      sd[0] += tb - ta; sd[1] += tc - tb; sd[2] += td - tc; sd[3] += te - td; sd[4] += tf - te;
+#endif
       inc(rs);
       inc(ws);
     }
   } else {
     int rs = 0, ws = 0;
     for (int s = 0; s < nsteps; ++s) {
+      DCX_SEGT(ta);
       readF(rs);  // MEM1(s): fragments of step s, issue step s + NS - 1 (s >= 1)
       if (s >= 1 && s + NS - 1 < nsteps) dma_step(s + NS - 1, ws);
+      DCX_SEGT(tb);
       wait_dma(in_flight(s + 2, s >= 1 ? s + NS - 1 : NS - 1));
+      DCX_SEGT(tc);
       seg_barrier();
+      DCX_SEGT(td);
       mfma();  // MFMA(s)
+      DCX_SEGT(te);
       seg_barrier();
+      DCX_SEGT(tf);
+#ifdef DCX_SEG_DIAG
+      sd[0] += te - td; sd[1] += tf - te; sd[2] += tb - ta; sd[3] += tc - tb; sd[4] += td - tc;
+#endif
       inc(rs);
       if (s >= 1) inc(ws);
       else ws = 0;
     }
   }
+#ifdef DCX_SEG_DIAG
+  if ((threadIdx.x & 255) == 0) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_seg_diag[group * 6 + i], sd[i]);
+    if (group == 0) atomicAdd(&g_seg_diag[12], (unsigned long long)nsteps);
+  }
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   epilogue_top2_q<BM, BN, 4, WN>(p, acc, q0, co0, nt, ntiles, reinterpret_cast<float*>(lds));
 }
@@ -3645,7 +3727,6 @@ hipError_t launch_splitk_epilogue(const ConvParams& p, const float* partials, in
   return hipGetLastError();
 }
 
-// DCX_BF16_REG_EPI=0 (read at each launch; A/B and tests): the LDS-staged epilogue for pwconv1 too
 // conv_gemm_bf16dp's GELU table: ConvParams::gelu_lut = the table offset from which a wave takes the
 // evaluated epilogue (2 kGeluN, the table's end).  DCX_GELU_LUT (read at each launch): 0 = evaluated
 // always (A/B); a smaller positive limit sends more waves through the evaluated epilogue (tests)
@@ -3668,6 +3749,7 @@ static int num_cus() {
   }
   return cus;
 }
+// DCX_BF16_REG_EPI=0 (read at each launch; A/B and tests): the LDS-staged epilogue for pwconv1 too
 static bool reg_epi_off() {
   const char* e = getenv("DCX_BF16_REG_EPI");
   return e && *e == '0';
@@ -3842,6 +3924,64 @@ hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t
     if (kname) *kname = "conv_gemm_x6dq_group<512,128,halo>";
     hipLaunchKernelGGL((conv_gemm_x6dq_group<128>), dim3((unsigned)start), dim3(512), 0, s, g);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_split_group(const ConvParams* ps, int n, int batch, hipStream_t s, const char** kname) {
+  if (n < 1 || n > kMaxGroup || batch < 1) return hipErrorInvalidValue;
+  for (int i = 0; i < n; ++i) {  // every member a conv launch_conv would give to conv_gemm_x6pp<64, 128>
+    const ConvParams& p = ps[i];
+    const int S = std::max(1, p.ksplit);
+    const int span = tap_span(p);
+    if (!p.x6 || !p.w6 || p.nprod != 6 || p.x_compact || p.Cout % 128 || p.Cin % BK || p.taps < 3 || span == 0 ||
+        span > 64 || (p.Cin / BK) * p.taps % 2 || (S > 1 && (p.kunit < 1 || (p.Cin / BK) % p.kunit ||
+                                                            (p.Cin / BK) / p.kunit < S)))
+      return hipErrorNotSupported;
+  }
+  int order[kMaxGroup] = {0, 1, 2};  // most work per slice first
+  auto work = [&](int i) { return (long long)ps[i].taps * (ps[i].Cin / BK) / std::max(1, ps[i].ksplit); };
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j)
+      if (work(order[j]) > work(order[i])) std::swap(order[i], order[j]);
+  ConvGroup g{};
+  long long start = 0;
+  for (int k = 0; k < n; ++k) {
+    const ConvParams& p = ps[order[k]];
+    g.p[k] = p;
+    g.p[k].batch = batch * std::max(1, p.ksplit);
+    g.p[k].phases = 1;
+    g.tiles_per_clip[k] = ((p.Lq + 255) / 256) * (p.Cout / 128);
+    g.start[k] = (int)start;
+    start += (long long)g.tiles_per_clip[k] * g.p[k].batch;
+  }
+  if (start > (1LL << 30)) return hipErrorInvalidValue;
+  for (int k = n; k <= kMaxGroup; ++k) g.start[k] = (int)start;
+  if (kname) *kname = "conv_gemm_x6pp_group<256,128,halo>";
+  hipLaunchKernelGGL(conv_gemm_x6pp_group, dim3((unsigned)start), dim3(512), 0, s, g);
+  return hipGetLastError();
+}
+
+hipError_t launch_splitk_epilogue_group(const ConvParams* ps, const float* const* partials, const int* splits,
+                                        const long long* strides, int n, int batch, hipStream_t s) {
+  if (n < 1 || n > kMaxGroup || batch < 1) return hipErrorInvalidValue;
+  SplitEpiGroup g{};
+  long long start = 0;
+  for (int k = 0; k < n; ++k) {
+    const ConvParams& p = ps[k];
+    if (splits[k] < 1 || p.Cout % 4 || p.ldy != p.Cout) return hipErrorInvalidValue;
+    g.p[k] = p;
+    g.p[k].batch = batch;
+    g.p[k].phases = 1;
+    g.part[k] = partials[k];
+    g.splits[k] = splits[k];
+    g.stride[k] = strides[k];
+    g.total4[k] = (long long)batch * p.Lq * (p.Cout / 4);
+    g.start[k] = (int)start;
+    start += (g.total4[k] + 255) / 256;
+  }
+  if (start > (1LL << 30)) return hipErrorInvalidValue;
+  for (int k = n; k <= kMaxGroup; ++k) g.start[k] = (int)start;
+  hipLaunchKernelGGL(splitk_epilogue_group_kernel, dim3((unsigned)start), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 

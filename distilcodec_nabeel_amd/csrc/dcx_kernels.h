@@ -90,6 +90,17 @@ struct ConvGroup {
   int tiles_per_clip[kMaxGroup];
 };
 
+// The reduces of a grouped split-K launch (launch_splitk_epilogue_group): member k's partials
+// part[k] (splits[k] slices, stride[k] floats apart) finished with p[k]'s epilogue by the blocks
+// [start[k], start[k + 1]), total4[k] 4-channel groups.
+struct SplitEpiGroup {
+  ConvParams p[kMaxGroup];
+  const float* part[kMaxGroup];
+  int splits[kMaxGroup];
+  long long stride[kMaxGroup], total4[kMaxGroup];
+  int start[kMaxGroup + 1];
+};
+
 // One pair (c1 dilated, c2 undilated) of each ResBlock1 of a small-channel ParallelBlock (C = 32 / 64,
 // x6 arithmetic), fused: silu(c1) stays in LDS (dcx_resblock.hip).  Member m reads state src[m]
 // ([clip][L][C] fp32) and writes src[m] + c2(silu(c1(silu(src[m])))) to dst[m] (dst != src: the
@@ -124,6 +135,13 @@ hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** k
 // whole epilogue (bias, epi, mean, every output and layout).
 hipError_t launch_splitk_epilogue(const ConvParams& p, const float* partials, int splits, long long stride, int batch,
                                   int phases, hipStream_t s);
+// Split-K latency mode, grouped (round 4): n <= kMaxGroup single-phase halo convs (ResBlock convs:
+// Cout % 128, taps >= 3), member k with its own ps[k].ksplit (1 = unsplit: the member's epilogue runs
+// in the conv) and virtual clips batch * ksplit, as one conv_gemm_x6pp launch; then one launch of
+// the reduces of the split members.  hipErrorNotSupported when the members do not qualify.
+hipError_t launch_conv_split_group(const ConvParams* ps, int n, int batch, hipStream_t s, const char** kname);
+hipError_t launch_splitk_epilogue_group(const ConvParams* ps, const float* const* partials, const int* splits,
+                                        const long long* strides, int n, int batch, hipStream_t s);
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname);
 int vq_argmin_ntiles(int ncodes);
 // per-row partial count of the x6 / bf16-mode prefilter launch_vq_prefilter runs for `rows` rows with

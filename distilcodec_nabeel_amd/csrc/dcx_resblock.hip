@@ -29,6 +29,7 @@
 // plane), so every ds_read_b128 of 16 consecutive rows of one piece is conflict-free at any tap
 // offset, and the weight slot is the global tap slice [chunk][Cout][96 B] copied as is.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "dcx_kernels.h"
@@ -70,9 +71,13 @@ __device__ unsigned long long g_rp_diag[32];  // [C == 64][16]
 #define RP_T(v)
 #endif
 
+// output rows per tile: 496 / 176 (C = 32 / 64) by default; the launcher takes fewer rows per tile
+// when a launch has too few tiles for the CUs (small batches: the C5 streaming hop), same bits
 template <int C>
+constexpr int kRpRows = C == 32 ? 496 : 176;
+template <int C, int RR = kRpRows<C>>
 struct RpGeom {
-  static constexpr int R = C == 32 ? 496 : 176;  // output rows per tile
+  static constexpr int R = RR;
   static constexpr int M1 = R + 16;              // c1 rows: [r0 - 8, r0 + R + 8)
   static constexpr int H1 = 32;                  // largest c1 reach (k - 1) / 2 * d
   static constexpr int NS = M1 + 2 * H1;         // S image rows
@@ -95,9 +100,9 @@ struct RpGeom {
 
 }  // namespace
 
-template <int C, bool MEAN>
+template <int C, bool MEAN, int RR = kRpRows<C>>
 __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
-  using G = RpGeom<C>;
+  using G = RpGeom<C, RR>;
   constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB1, BLK = G::BLK, IMG = G::IMG, TPS = G::TPS;
   constexpr int WTAP = G::WTAP, WSLOT = G::WSLOT, G8 = G::G8, NIT = G::NIT, WP = G::WP, WPW = G::WPW, NS = G::NS;
   __shared__ __attribute__((aligned(16))) char lds[G::LDS];
@@ -414,9 +419,9 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
 // of the next tap in the stream (next conv, member or tile).  The tap loops need no barrier; only the
 // image hand-offs do (S -> T after c1, T -> the next S after c2).  Arithmetic, summation order and
 // layouts are conv_res_pair's, so the results are the same bits.
-template <int C, bool MEAN>
+template <int C, bool MEAN, int RR = kRpRows<C>>
 __global__ void __launch_bounds__(512, 1) conv_res_pair_g(const ResPairParams p) {
-  using G = RpGeom<C>;
+  using G = RpGeom<C, RR>;
   constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB1, BLK = G::BLK, IMG = G::IMG;
   constexpr int G8 = G::G8, NIT = G::NIT, NS = G::NS, WTAP = G::WTAP;
   __shared__ __attribute__((aligned(16))) char lds[IMG + 2 * kMaxGroup * C * 4];
@@ -700,9 +705,6 @@ hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** k
         !p.w1[m] || !p.w2[m] || !p.b1[m] || !p.b2[m] || (!p.mean_out && !p.dst[m]))
       return hipErrorInvalidValue;
   }
-  const int R = p.C == 32 ? RpGeom<32>::R : RpGeom<64>::R;
-  const long long total = (long long)((p.L + R - 1) / R) * p.batch;
-  if (total > (1LL << 30)) return hipErrorInvalidValue;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -710,6 +712,29 @@ hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** k
         cus < 1)
       return hipErrorInvalidValue;
   }
+  // rows per tile: the default unless a smaller tile finishes the launch sooner, by rounds of tiles
+  // over the CUs times a tile's rows (c1 rows R + 16, c2 rows R, ~64 rows' worth of fixed cost);
+  // DCX_RP_R (read at each launch; tests) forces one of the instantiated sizes
+  static constexpr int kSizes32[3] = {496, 240, 112}, kSizes64[3] = {176, 112, 48};
+  const int* sizes = p.C == 32 ? kSizes32 : kSizes64;
+  int R = sizes[0];
+  long long best = -1;
+  for (int i = 0; i < 3; ++i) {
+    const int r = sizes[i];
+    const long long tiles = (long long)((p.L + r - 1) / r) * p.batch;
+    const long long cost = (tiles + cus - 1) / cus * (2LL * r + 16 + 64);
+    if (best < 0 || cost < best) {
+      best = cost;
+      R = r;
+    }
+  }
+  if (const char* fr = getenv("DCX_RP_R")) {
+    const int r = std::atoi(fr);
+    for (int i = 0; i < 3; ++i)
+      if (sizes[i] == r) R = r;
+  }
+  const long long total = (long long)((p.L + R - 1) / R) * p.batch;
+  if (total > (1LL << 30)) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)std::min<long long>(total, cus);  // one workgroup per CU (LDS)
   // C = 32: the barrier-free kernel (A/B in one session: 12.4 vs 12.9 ms per C2 generator);
   // C = 64: the step schedule, which measured faster there (22.3 vs 23.2 ms).
@@ -722,27 +747,32 @@ hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** k
   const char* sy = getenv("DCX_RP_SYNC");
   ResPairParams q = p;
   q.tap_sync = sy && *sy ? std::max(0, std::atoi(sy)) : 0;
-  if (p.C == 32 && !old) {
-    if (kname) *kname = p.mean_out ? "conv_res_pair_g<32,mean>" : "conv_res_pair_g<32>";
-    if (p.mean_out) hipLaunchKernelGGL((conv_res_pair_g<32, true>), dim3(grid), dim3(512), 0, s, q);
-    else hipLaunchKernelGGL((conv_res_pair_g<32, false>), dim3(grid), dim3(512), 0, s, q);
-    return hipGetLastError();
-  }
-  if (p.C == 64 && !old && g64 && *g64 == '1') {
-    if (kname) *kname = p.mean_out ? "conv_res_pair_g<64,mean>" : "conv_res_pair_g<64>";
-    if (p.mean_out) hipLaunchKernelGGL((conv_res_pair_g<64, true>), dim3(grid), dim3(512), 0, s, q);
-    else hipLaunchKernelGGL((conv_res_pair_g<64, false>), dim3(grid), dim3(512), 0, s, q);
-    return hipGetLastError();
-  }
-  if (p.C == 32) {
-    if (kname) *kname = p.mean_out ? "conv_res_pair<32,mean>" : "conv_res_pair<32>";
-    if (p.mean_out) hipLaunchKernelGGL((conv_res_pair<32, true>), dim3(grid), dim3(512), 0, s, p);
-    else hipLaunchKernelGGL((conv_res_pair<32, false>), dim3(grid), dim3(512), 0, s, p);
-  } else {
-    if (kname) *kname = p.mean_out ? "conv_res_pair<64,mean>" : "conv_res_pair<64>";
-    if (p.mean_out) hipLaunchKernelGGL((conv_res_pair<64, true>), dim3(grid), dim3(512), 0, s, p);
-    else hipLaunchKernelGGL((conv_res_pair<64, false>), dim3(grid), dim3(512), 0, s, p);
-  }
+  static char names[64];
+  auto launch = [&](auto kern, const char* base, const ResPairParams& a) {
+    if (kname) {
+      snprintf(names, sizeof names, "%s%s%s", base, p.mean_out ? ",mean" : "", R == sizes[0] ? ">" : ",small>");
+      *kname = names;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, s, a);
+  };
+#define DCX_RP_LAUNCH(KERN, CC, A)                                                                       \
+  do {                                                                                                   \
+    const char* base_ = #KERN "<" #CC;                                                                   \
+    if (R == sizes[0]) {                                                                                 \
+      if (p.mean_out) launch(KERN<CC, true>, base_, A); else launch(KERN<CC, false>, base_, A);          \
+    } else if (R == sizes[1]) {                                                                          \
+      if (p.mean_out) launch(KERN<CC, true, (CC == 32 ? 240 : 112)>, base_, A);                          \
+      else launch(KERN<CC, false, (CC == 32 ? 240 : 112)>, base_, A);                                    \
+    } else {                                                                                             \
+      if (p.mean_out) launch(KERN<CC, true, (CC == 32 ? 112 : 48)>, base_, A);                           \
+      else launch(KERN<CC, false, (CC == 32 ? 112 : 48)>, base_, A);                                     \
+    }                                                                                                    \
+  } while (0)
+  if (p.C == 32 && !old) DCX_RP_LAUNCH(conv_res_pair_g, 32, q);
+  else if (p.C == 64 && !old && g64 && *g64 == '1') DCX_RP_LAUNCH(conv_res_pair_g, 64, q);
+  else if (p.C == 32) DCX_RP_LAUNCH(conv_res_pair, 32, p);
+  else DCX_RP_LAUNCH(conv_res_pair, 64, p);
+#undef DCX_RP_LAUNCH
   return hipGetLastError();
 }
 

@@ -95,3 +95,27 @@ def test_unit_pipeline_same_bits_as_step_schedule(engines, B, T):
     torch.cuda.synchronize()
     assert torch.isfinite(a).all()
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,T", [(1, 93), (2, 31), (1, 7)])
+def test_tile_rows_same_bits(engines, B, T):
+    """The pair kernels on smaller tiles (round 4: 240 / 112 rows at C = 32, 112 / 48 at C = 64, which
+    the launcher takes when the default 496 / 176 leave most CUs idle, e.g. the C5 hop): every
+    output row is computed with the same arithmetic whatever the tile, so every size (DCX_RP_R, read
+    at each launch) gives the same bits as the default on both the step-schedule and the
+    barrier-free kernels."""
+    fused, _ = engines
+    z = _z(B, T, 500 + T)
+    outs = []
+    for r in ("496", "240", "112", "176", "48"):
+        for old in ("0", "1"):
+            os.environ["DCX_RP_R"] = r
+            os.environ["DCX_RP_OLD"] = old
+            try:
+                outs.append(fused.generate(z))
+            finally:
+                del os.environ["DCX_RP_R"], os.environ["DCX_RP_OLD"]
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0]).all()
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)

@@ -82,3 +82,34 @@ def test_graph_hop_on_split_engine(engines):
     codes, wav = codes.clone(), wav.clone()
     c2, w2 = split.encode_decode(torch.nn.functional.pad(x, (1, 0)))
     assert torch.equal(codes, c2) and torch.equal(wav, w2)
+
+
+@pytest.mark.parametrize("T", [24, 93])
+def test_grouped_split_launches(engines, cfg, state, T):
+    """The three ResBlocks' convs of one dilation index as one grouped split-K launch plus one
+    grouped reduce (round 4): the grouped kernel runs (profile), the generator output is within the
+    fp32 summation-order distance of the per-conv split launches (DCX_SPLIT_GROUP_OFF=1, read at
+    each call) and of the fp64 oracle (>= 80 dB)."""
+    import os
+
+    from oracle import reference_cpu as R
+
+    split, _ = engines
+    g = torch.Generator().manual_seed(100 + T)
+    z = torch.randn(1, T, 1024, generator=g) * 0.5
+    split.profile(True)
+    split.profile_reset()
+    wav = split.generate(z).cpu().reshape(-1)
+    names = split.profile_read()
+    split.profile(False)
+    assert any("x6pp_group" in k for k in names), sorted(names)
+    os.environ["DCX_SPLIT_GROUP_OFF"] = "1"
+    try:
+        wav_single = split.generate(z).cpu().reshape(-1)
+    finally:
+        del os.environ["DCX_SPLIT_GROUP_OFF"]
+    with torch.no_grad():
+        ref = R.generator(z.transpose(1, 2).double(), state["generator"], cfg["decoder"], torch.float64).reshape(-1)
+    s1, s2 = _snr(wav, ref), _snr(wav, wav_single)
+    print(f"T={T}: grouped split-K vs fp64 oracle {s1:.1f} dB, vs per-conv split {s2:.1f} dB")
+    assert s1 >= 80 and s2 >= 100

@@ -210,3 +210,4 @@ def test_rescore_in_place_path_same_codes(veng, cfg, state, per_row):
     rows, _ = inplace.vq_rescore_stats()
     assert rows > 0
     assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
+
