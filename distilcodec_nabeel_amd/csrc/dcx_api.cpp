@@ -736,6 +736,16 @@ int run_conv_group_split(dcx_codec* h, const ConvW* const* w, const ConvCall* c,
   if (n < 2 || std::getenv("DCX_SPLIT_GROUP_OFF")) return 1;
   long long tiles[dcx::kMaxGroup], out[dcx::kMaxGroup], chunks[dcx::kMaxGroup];
   int S[dcx::kMaxGroup], smax[dcx::kMaxGroup];
+  // a ParallelBlock's last convs (the mean folded into their epilogues) must all be split, so that
+  // one reduce thread finishes every member of an element in ResBlock order
+  const bool chain = p[0].mean_mode != dcx::MEAN_NONE;
+  if (chain) {
+    if (p[0].mean_mode != dcx::MEAN_FIRST || p[n - 1].mean_mode != dcx::MEAN_LAST) return 1;
+    for (int i = 1; i < n - 1; ++i)
+      if (p[i].mean_mode != dcx::MEAN_MID) return 1;
+    for (int i = 1; i < n; ++i)
+      if (p[i].macc != p[0].macc || c[i].Lq != c[0].Lq || w[i]->cout != w[0]->cout) return 1;
+  }
   long long total = 0;
   for (int i = 0; i < n; ++i) {
     if (split_factor(h, *w[i], c[i], p[i]) < 2 || w[i]->taps < 3 || w[i]->out_mul != 1) return 1;
@@ -744,9 +754,11 @@ int run_conv_group_split(dcx_codec* h, const ConvW* const* w, const ConvCall* c,
     const int unit = w[i]->taps % 2 ? 2 : 1;
     chunks[i] = (long long)w[i]->taps * (w[i]->cin / 16);
     smax[i] = (int)std::min<long long>(kSplitMax, (w[i]->cin / 16) / unit);
-    S[i] = 1;
-    total += tiles[i];
+    S[i] = chain ? 2 : 1;
+    if (S[i] > smax[i]) return 1;
+    total += S[i] * tiles[i];
   }
+  if (total > 256) return 1;
   // K slices: repeatedly give one more slice to the member whose slices are longest, while the
   // grid stays within one workgroup per CU
   for (;;) {
@@ -795,7 +807,7 @@ int run_conv_group_split(dcx_codec* h, const ConvW* const* w, const ConvCall* c,
   const hipError_t e = dcx::launch_conv_split_group(q, n, c[0].batch, s, &kname);
   if (e == hipErrorNotSupported) return 1;
   HIPCHK(h, e);
-  if (nr) HIPCHK(h, dcx::launch_splitk_epilogue_group(r, part, rs, rstride, nr, c[0].batch, s));
+  if (nr) HIPCHK(h, dcx::launch_splitk_epilogue_group(r, part, rs, rstride, nr, c[0].batch, chain, s));
   ps.done((std::string("splitk:") + kname).c_str(), fl, by);
   return DCX_OK;
 }
@@ -1257,8 +1269,11 @@ int run_parallel_block(dcx_codec* h, int i, int B, int Lo, const PBlockBufs& b, 
       }
       RUN(run_conv_group(h, w2, c2, c.n_res, s));
     } else {  // last pair: ParallelBlock mean folded into the epilogues, in ResBlock order
+      const ConvW* w2[NR];
+      ConvCall cm[NR];
       for (int rb = 0; rb < c.n_res; ++rb) {
-        ConvCall cc = framed(b.Tb_in[rb], B, Lo, Co);
+        ConvCall& cc = cm[rb];
+        cc = framed(b.Tb_in[rb], B, Lo, Co);
         cc.epi = dcx::EPI_RES;
         cc.res = b.R[rb];
         cc.macc = b.Mx;
@@ -1268,8 +1283,24 @@ int run_parallel_block(dcx_codec* h, int i, int B, int Lo, const PBlockBufs& b, 
           if (b.last) cc.y2 = b.Mx;
           else cc.silu_to(b.next);  // input of the next ConvT
         }
-        RUN(run_conv(h, h->res[i][rb][ci][1], cc, s));
+        w2[rb] = &h->res[i][rb][ci][1];
       }
+      // split-K mode: one grouped launch and one chained reduce; otherwise conv by conv (the
+      // mean's order forbids the grouped unsplit kernel)
+      int rc = 1;
+      if (h->split_k >= 2 && c.n_res > 1) {
+        ConvParams p[NR];
+        double fl = 0, by = 0;
+        for (int rb = 0; rb < c.n_res; ++rb) {
+          RUN(conv_params(h, *w2[rb], cm[rb], false, p[rb]));
+          fl += conv_flops(*w2[rb], cm[rb]);
+          by += conv_bytes(*w2[rb], cm[rb]);
+        }
+        rc = run_conv_group_split(h, w2, cm, p, c.n_res, fl, by, s);
+      }
+      if (rc != 1) RUN(rc);
+      else
+        for (int rb = 0; rb < c.n_res; ++rb) RUN(run_conv(h, *w2[rb], cm[rb], s));
     }
   }
   return DCX_OK;

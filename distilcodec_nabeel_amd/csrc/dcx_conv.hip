@@ -560,6 +560,12 @@ __global__ void __launch_bounds__(256) splitk_epilogue_group_kernel(const SplitE
   const int k = t >= g.start[1] ? (t >= g.start[2] ? 2 : 1) : 0;
   const long long i4 = (long long)(t - g.start[k]) * 256 + threadIdx.x;
   if (i4 >= g.total4[k]) return;
+  if (g.chain) {  // g.chain members, one range of blocks (member 0's), every member in order
+    splitk_epi4(g.p[0], g.part[0], g.splits[0], g.stride[0], i4);
+    if (g.chain > 1) splitk_epi4(g.p[1], g.part[1], g.splits[1], g.stride[1], i4);
+    if (g.chain > 2) splitk_epi4(g.p[2], g.part[2], g.splits[2], g.stride[2], i4);
+    return;
+  }
   if (k == 0) splitk_epi4(g.p[0], g.part[0], g.splits[0], g.stride[0], i4);
   else if (k == 1) splitk_epi4(g.p[1], g.part[1], g.splits[1], g.stride[1], i4);
   else splitk_epi4(g.p[2], g.part[2], g.splits[2], g.stride[2], i4);
@@ -3962,9 +3968,10 @@ hipError_t launch_conv_split_group(const ConvParams* ps, int n, int batch, hipSt
 }
 
 hipError_t launch_splitk_epilogue_group(const ConvParams* ps, const float* const* partials, const int* splits,
-                                        const long long* strides, int n, int batch, hipStream_t s) {
+                                        const long long* strides, int n, int batch, bool chain, hipStream_t s) {
   if (n < 1 || n > kMaxGroup || batch < 1) return hipErrorInvalidValue;
   SplitEpiGroup g{};
+  g.chain = chain ? n : 0;
   long long start = 0;
   for (int k = 0; k < n; ++k) {
     const ConvParams& p = ps[k];
@@ -3976,8 +3983,11 @@ hipError_t launch_splitk_epilogue_group(const ConvParams* ps, const float* const
     g.splits[k] = splits[k];
     g.stride[k] = strides[k];
     g.total4[k] = (long long)batch * p.Lq * (p.Cout / 4);
+    if (chain && (p.Lq != ps[0].Lq || p.Cout != ps[0].Cout)) return hipErrorInvalidValue;
     g.start[k] = (int)start;
-    start += (g.total4[k] + 255) / 256;
+    // chain: one range of blocks (member 0's) whose threads finish every member in order; the
+    // other members' ranges are empty but start[] still marks which members exist
+    start += chain && k > 0 ? 0 : (g.total4[k] + 255) / 256;
   }
   if (start > (1LL << 30)) return hipErrorInvalidValue;
   for (int k = n; k <= kMaxGroup; ++k) g.start[k] = (int)start;

@@ -99,6 +99,11 @@ struct SplitEpiGroup {
   int splits[kMaxGroup];
   long long stride[kMaxGroup], total4[kMaxGroup];
   int start[kMaxGroup + 1];
+  // chain (> 0: the member count): the members are a ParallelBlock's last convs with the mean folded
+  // into their epilogues (MEAN_FIRST, MID.., LAST on one accumulator); one thread finishes an element
+  // of every member in member order, so the mean is accumulated in ResBlock order as the per-conv
+  // reduces do
+  int chain;
 };
 
 // One pair (c1 dilated, c2 undilated) of each ResBlock1 of a small-channel ParallelBlock (C = 32 / 64,
@@ -141,7 +146,7 @@ hipError_t launch_splitk_epilogue(const ConvParams& p, const float* partials, in
 // the reduces of the split members.  hipErrorNotSupported when the members do not qualify.
 hipError_t launch_conv_split_group(const ConvParams* ps, int n, int batch, hipStream_t s, const char** kname);
 hipError_t launch_splitk_epilogue_group(const ConvParams* ps, const float* const* partials, const int* splits,
-                                        const long long* strides, int n, int batch, hipStream_t s);
+                                        const long long* strides, int n, int batch, bool chain, hipStream_t s);
 hipError_t launch_vq_argmin(const ConvParams& p, int rows, hipStream_t s, const char** kname);
 int vq_argmin_ntiles(int ncodes);
 // per-row partial count of the x6 / bf16-mode prefilter launch_vq_prefilter runs for `rows` rows with
