@@ -650,6 +650,34 @@ __device__ __forceinline__ void top2_merge(float& v1, int& i1, float& v2, float 
   }
 }
 
+// top2_merge as selects (no divergent branch: the epilogues run it on every lane), same results
+__device__ __forceinline__ void top2_merge_sel(float& v1, int& i1, float& v2, float ov1, int oi1, float ov2) {
+  const bool take = (ov1 < v1) | ((ov1 == v1) & (oi1 < i1));  // (bitwise: no short-circuit branch)
+  const float nv2 = take ? fminf(v1, ov2) : fminf(v2, ov1);
+  v1 = take ? ov1 : v1;
+  i1 = take ? oi1 : i1;
+  v2 = nv2;
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, dpp_i<CTRL>(__builtin_bit_cast(int, v)));
+}
+template <int CTRL>
+__device__ __forceinline__ void top2_dpp_step(float& v1, int& i1, float& v2) {
+  top2_merge_sel(v1, i1, v2, dpp_f<CTRL>(v1), dpp_i<CTRL>(i1), dpp_f<CTRL>(v2));
+}
+// the top 2 over the 16 lanes of a DPP row (lanes 16 k .. 16 k + 15), left in every lane of it: quad
+// xor 1, quad xor 2 (quad_perm), then the half-row mirror (quad 0 <-> 1, 2 <-> 3) and the row mirror
+// (the two halves); VALU moves instead of four ds_bpermute round trips per value
+__device__ __forceinline__ void top2_row16(float& v1, int& i1, float& v2) {
+  top2_dpp_step<0xB1>(v1, i1, v2);   // quad_perm [1, 0, 3, 2]
+  top2_dpp_step<0x4E>(v1, i1, v2);   // quad_perm [2, 3, 0, 1]
+  top2_dpp_step<0x141>(v1, i1, v2);  // row_half_mirror
+  top2_dpp_step<0x140>(v1, i1, v2);  // row_mirror
+}
+
 template <int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void epilogue_top2(const ConvParams& p, f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int q0,
                                               int co0, int nt, int ntiles, float* smem) {
@@ -3300,13 +3328,15 @@ __device__ __forceinline__ void epilogue_top2_q(const ConvParams& p, f32x4 (&acc
       int i1 = 0x7fffffff;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
+        // a lane's codes come in increasing order, so a strict < keeps the lowest index on ties; the
+        // second smallest is min(v2, max(v1, d2)) (top2_merge with one new value, in 5 VALU ops)
         const int co = co0 + wn * WC + j * 16 + lc;
         const float d2 = (xx + e2v[j]) + (-2.0f * acc[i][j][r]);
-        top2_merge(v1, i1, v2, d2, co, __builtin_inff());
+        i1 = d2 < v1 ? co : i1;
+        v2 = fminf(v2, fmaxf(v1, d2));
+        v1 = fminf(v1, d2);
       }
-#pragma unroll
-      for (int off = 8; off >= 1; off >>= 1)
-        top2_merge(v1, i1, v2, __shfl_xor(v1, off, 64), __shfl_xor(i1, off, 64), __shfl_xor(v2, off, 64));
+      top2_row16(v1, i1, v2);
       if (lc == 0) {
         rv[wn * BM + rloc] = v1;
         rv2[wn * BM + rloc] = v2;
@@ -3502,6 +3532,7 @@ template <int NS>
 __global__ void __launch_bounds__(512, 2) vq_prefilter_b1(const ConvParams p) {
   constexpr int BM = 256, BN = 256, WN = 2;
   constexpr int WR = BM / 4, WC = BN / 2, TM = WR / 16, TN = WC / 16;
+  DCX_TILET(tile_t0);
   constexpr int RW = 32;                       // ushorts per LDS row (64 bytes)
   constexpr int A_G = BM * 4 / 64 / 2;         // DMA instructions per group per tile (8)
   constexpr int B_G = BN * 4 / 64 / 2;         // (8)
@@ -3604,6 +3635,10 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_b1(const ConvParams p) {
   for (int t = 0; t < NS && t < nsteps; ++t) dma_step(t, t);
   // group 0 reads step 0 now and step 1 in segment 1 (its own MFMA segment 0 comes first)
   wait_dma(group == 0 ? in_flight(2, NS - 1) : in_flight(1, NS - 1));
+#ifdef DCX_TILE_DIAG
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (timing build: the prologue's DMA landed)
+#endif
+  DCX_TILET(tile_t1);
 #ifdef DCX_VQ_STATICPRIO
   if (group == 1) __builtin_amdgcn_s_setprio(1);
 #endif
@@ -3664,7 +3699,22 @@ __global__ void __launch_bounds__(512, 2) vq_prefilter_b1(const ConvParams p) {
   }
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  DCX_TILET(tile_t2);
   epilogue_top2_q<BM, BN, 4, WN>(p, acc, q0, co0, nt, ntiles, reinterpret_cast<float*>(lds));
+#ifdef DCX_TILE_DIAG
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+    const unsigned int k = atomicAdd(&g_tile_cnt, 1u);
+    if (k < (unsigned)kTileDiagMax) {
+      unsigned long long* o = g_tile_diag + 6ull * k;
+      o[0] = tile_t0; o[1] = tile_t1; o[2] = tile_t2; o[3] = t3;
+      o[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      o[5] = __builtin_amdgcn_s_getreg((15 << 11) | 20) | ((unsigned long long)nsteps << 16);
+    }
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
