@@ -237,3 +237,23 @@ def test_c1_reference_demo_mp3(codec, state, cfg):
     check_codes(codes, rc, dec)
     wav = codec.decode_from_codes(codes[0].tolist(), minus_token_offset=False)
     check_wave(codec._engine(), codes, rc, wav[:, 0], ref["wav"][:, 0].numpy(), 80)
+
+
+def test_c_abi_decode_counts_out_of_range_codes(codec):
+    """dcx_vq_decode (the C ABI under the Python guards): codes outside [0, codebook_size) other than
+    the masked code -1 read row 0 and are counted into n_invalid, codebook_size itself included
+    (round-3 ADVICE: it must not read the masked bias row); -1 and wrapped negatives are valid."""
+    eng = codec._engine()
+    codes = torch.tensor([[5, 32768, -1, 40000, -32768, 7, 32767, -32769]], dtype=torch.int32, device="cuda")
+    z = torch.empty(1, codes.shape[1], eng.D, device="cuda")
+    n_invalid = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ws = eng.workspace(1, codes.shape[1])
+    eng._check(eng.L.dcx_vq_decode(eng.h, eng._ptr(codes), 1, codes.shape[1], eng._ptr(z), eng._ptr(n_invalid),
+                                   eng._ptr(ws), ws.numel(), eng._stream()))
+    torch.cuda.synchronize()
+    assert int(n_invalid.item()) == 3  # 32768, 40000, -32769
+    ref0 = eng.vq_decode(torch.tensor([[0]], dtype=torch.int32, device="cuda"))[0, 0]
+    for i in (1, 3, 7):
+        assert torch.equal(z[0, i], ref0)
+    masked = eng.vq_decode(torch.tensor([[-1]], dtype=torch.int32, device="cuda"))[0, 0]
+    assert torch.equal(z[0, 2], masked) and not torch.equal(z[0, 1], masked)
