@@ -2067,7 +2067,8 @@ size_t dcx_module_workspace_size(const dcx_codec* h, const char* module, int32_t
   if (!h || !module || batch <= 0 || rows <= 0 || !h->finalized) return 0;
   Bump d(nullptr, 0, true);
   if (stage_module(const_cast<dcx_codec*>(h), module, nullptr, batch, (int)rows, nullptr, d, 0) != DCX_OK) return 0;
-  return d.off + 4096;
+  // the split-K partial sums, carved ahead of the module's buffers (STAGE_PRE)
+  return d.off + 4096 + (h->split_k > 1 ? kSplitScratch + 256 : 0);
 }
 
 int dcx_module_forward(dcx_codec* h, const char* module, const float* x, int32_t batch, int64_t rows,

@@ -187,3 +187,16 @@ def test_dwconv_run_same_bits_as_tiled(cfg, state, gemm, B, secs):
         del os.environ["DCX_DWCONV_TILED"]
     assert torch.isfinite(a).all()
     assert torch.equal(a, b)
+
+
+def test_module_in_split_k_mode(cfg, state, golden):
+    """dcx_module_workspace_size counts the split-K partial-sum scratch that every stage call carves
+    ahead of its buffers when the latency mode is on (round 4: without it a module call in that mode
+    failed with 'workspace too small'); the split ConvNeXt block stays within the module tolerance."""
+    from distilcodec_nabeel_amd.engine import NativeCodec
+
+    e = NativeCodec(cfg, state, "cuda:0", gemm="x6", with_generator=False)
+    e.set_split_k(16)
+    m = golden["modules"]
+    y = e.module("encoder.stages.0.0", _cl(m["convnext256_in"]))
+    assert _rel(_cf(y), m["convnext256_out"]) < 2e-4
