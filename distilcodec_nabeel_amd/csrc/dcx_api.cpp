@@ -666,6 +666,10 @@ int split_factor(const dcx_codec* h, const ConvW& w, const ConvCall& c, const Co
   // rule would pick unsplit: in this mode the bits depend on the split anyway)
   const long long tiles = (long long)c.batch * ((c.Lq + 255) / 256) * std::max(1, w.cout / 128) * w.phases;
   if (tiles >= 128) return 1;
+  // DCX_SPLIT_MIN_STEPS (read per call; A/B): convs with fewer K steps (taps x 16-channel chunks)
+  // run unsplit
+  if (const char* e = std::getenv("DCX_SPLIT_MIN_STEPS"))
+    if ((long long)w.taps * (w.cin / 16) < atoll(e)) return 1;
   const int unit = w.taps % 2 ? 2 : 1;  // chunks per slice: an even number of steps per slice
   const long long nunits = (w.cin / 16) / unit;
   return (int)std::min<long long>({(long long)std::min(h->split_k, kSplitMax), std::max<long long>(1, 256 / tiles), nunits});
