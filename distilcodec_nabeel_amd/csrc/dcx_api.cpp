@@ -132,6 +132,9 @@ struct dcx_codec {
   // points there only for the duration of one stage call (CallScope), which `busy` makes exclusive.
   int split_k = 0;
   float* split_buf = nullptr;
+  // A/B and test switches, read from the environment once at dcx_create (knobs_from_env) and changed
+  // only by dcx_set_knob; every launcher gets them through its parameters
+  dcx::Knobs knobs;
   std::atomic<int> busy{0};
 
   ConvW conv_pre;
@@ -586,6 +589,32 @@ struct ConvCall {
 // staging; conv_gemm_x6w8 AF32).
 bool f32_input_ok(const ConvW& w) { return w.cin <= 128 && w.cout <= 64 && w.taps >= 2; }
 
+// ---- A/B and test switches (dcx::Knobs): names are the environment variables dcx_create reads ----
+int* knob_slot(dcx::Knobs& k, const std::string& n) {
+  if (n == "DCX_RP_R") return &k.rp_rows;
+  if (n == "DCX_RP_OLD") return &k.rp_old;
+  if (n == "DCX_RP_G64") return &k.rp_g64;
+  if (n == "DCX_RP_SYNC") return &k.rp_sync;
+  if (n == "DCX_RP_W4") return &k.rp_w4;
+  if (n == "DCX_GELU_LUT") return &k.gelu_lut;
+  if (n == "DCX_BF16_PERSIST") return &k.bf16_persist;
+  if (n == "DCX_BF16_REG_EPI") return &k.bf16_reg_epi;
+  if (n == "DCX_DWCONV_TILED") return &k.dwconv_tiled;
+  if (n == "DCX_SPLIT_MIN_STEPS") return &k.split_min_steps;
+  if (n == "DCX_SPLIT_GROUP_OFF") return &k.split_group_off;
+  return nullptr;
+}
+
+void knobs_from_env(dcx::Knobs& k) {
+  static const char* const names[] = {"DCX_RP_R",         "DCX_RP_OLD",       "DCX_RP_G64",       "DCX_RP_SYNC",
+                                      "DCX_RP_W4",        "DCX_GELU_LUT",     "DCX_BF16_PERSIST", "DCX_BF16_REG_EPI",
+                                      "DCX_DWCONV_TILED", "DCX_SPLIT_MIN_STEPS", "DCX_SPLIT_GROUP_OFF"};
+  for (const char* n : names) {
+    const char* e = std::getenv(n);
+    if (e && *e) *knob_slot(k, n) = std::atoi(e);
+  }
+}
+
 int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32, ConvParams& p) {
   const bool x6 = x6_mode(h) && !force_f32;
   const bool x6_f32in = x6 && !c.x.p && c.x.f && f32_input_ok(w);
@@ -627,6 +656,7 @@ int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32,
   p.x_compact = x6 && c.x.p && c.x.c1 ? 1 : 0;
   p.y_compact = c.y6 ? c.y6c : 0;
   p.wc = one && h->compact ? w.wc : nullptr;
+  p.kn = &h->knobs;
   // compact inputs only feed one-product GEMMs; a compact output (the RNE hi value) may also be written
   // in x6 mode (x_pjt_in for vq_prefilter_b1)
   if (p.x_compact == 1 && !one) return fail(h, DCX_ERR_STATE, "internal: compact layout outside bf16 mode");
@@ -666,10 +696,9 @@ int split_factor(const dcx_codec* h, const ConvW& w, const ConvCall& c, const Co
   // rule would pick unsplit: in this mode the bits depend on the split anyway)
   const long long tiles = (long long)c.batch * ((c.Lq + 255) / 256) * std::max(1, w.cout / 128) * w.phases;
   if (tiles >= 128) return 1;
-  // DCX_SPLIT_MIN_STEPS (read per call; A/B): convs with fewer K steps (taps x 16-channel chunks)
-  // run unsplit
-  if (const char* e = std::getenv("DCX_SPLIT_MIN_STEPS"))
-    if ((long long)w.taps * (w.cin / 16) < atoll(e)) return 1;
+  // Knobs::split_min_steps (DCX_SPLIT_MIN_STEPS; A/B): convs with fewer K steps (taps x 16-channel
+  // chunks) run unsplit
+  if ((long long)w.taps * (w.cin / 16) < h->knobs.split_min_steps) return 1;
   const int unit = w.taps % 2 ? 2 : 1;  // chunks per slice: an even number of steps per slice
   const long long nunits = (w.cin / 16) / unit;
   return (int)std::min<long long>({(long long)std::min(h->split_k, kSplitMax), std::max<long long>(1, 256 / tiles), nunits});
@@ -737,7 +766,7 @@ int run_conv(dcx_codec* h, const ConvW& w, const ConvCall& c, hipStream_t s, boo
 // group does not qualify (the caller splits the members one by one).
 int run_conv_group_split(dcx_codec* h, const ConvW* const* w, const ConvCall* c, ConvParams* p, int n, double fl,
                          double by, hipStream_t s) {
-  if (n < 2 || std::getenv("DCX_SPLIT_GROUP_OFF")) return 1;
+  if (n < 2 || h->knobs.split_group_off) return 1;
   long long tiles[dcx::kMaxGroup], out[dcx::kMaxGroup], chunks[dcx::kMaxGroup];
   int S[dcx::kMaxGroup], smax[dcx::kMaxGroup];
   // a ParallelBlock's last convs (the mean folded into their epilogues) must all be split, so that
@@ -757,7 +786,8 @@ int run_conv_group_split(dcx_codec* h, const ConvW* const* w, const ConvCall* c,
     out[i] = (long long)c[i].batch * p[i].y_bstride;
     const int unit = w[i]->taps % 2 ? 2 : 1;
     chunks[i] = (long long)w[i]->taps * (w[i]->cin / 16);
-    smax[i] = (int)std::min<long long>(kSplitMax, (w[i]->cin / 16) / unit);
+    // at most the handle's split_k slices per member (dcx_set_split_k), as split_factor allows
+    smax[i] = (int)std::min<long long>(std::min(h->split_k, kSplitMax), (w[i]->cin / 16) / unit);
     S[i] = chain ? 2 : 1;
     if (S[i] > smax[i]) return 1;
     total += S[i] * tiles[i];
@@ -911,7 +941,7 @@ int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, in
   hid.c1 = hid.p && takes_compact(h, bw.pw2, M);
   LAUNCH(h, s, "dwconv_ln", 14.0 * M * C, 8.0 * M * C,
          dcx::launch_dwconv_ln(x, ln.f, ln.p, ln.c1 ? 1 : 0, bw.dww, bw.dwb, bw.ln.w, bw.ln.b, B, T, C,
-                               h->gemm_mode == DCX_GEMM_BF16 ? 1 : 0, s));
+                               h->gemm_mode == DCX_GEMM_BF16 ? 1 : 0, &h->knobs, s));
   ConvCall c1 = pointwise(ln, M);
   c1.out_to(hid);
   c1.epi = dcx::EPI_GELU;
@@ -1242,6 +1272,7 @@ int run_parallel_block(dcx_codec* h, int i, int B, int Lo, const PBlockBufs& b, 
       rp.L = Lo;
       rp.batch = B;
       rp.C = Co;
+      rp.kn = &h->knobs;
       ProfScope ps(h, s);
       const char* kname = "conv_res_pair";
       HIPCHK(h, dcx::launch_res_pair(rp, s, &kname));
@@ -1548,7 +1579,10 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
   if (m == "quantizer.search") {
     if (!h->codebook) return fail(h, DCX_ERR_STATE, "module weights not finalized");
     const int CD = c.codebook_dim, NC = c.codebook_size;
-    if (h->gemm_mode == DCX_GEMM_BF16) return fail(h, DCX_ERR_INVALID_ARG, "quantizer.search takes x6 or fp32 arithmetic");
+    // bf16 mode: the pipeline's search (compact bf16 x_pjt_in for the one-product prefilter, exact fp64
+    // rescore of x as given).  The reference searches x.float() with autocast off
+    // (vector_quantize_pytorch.py:462-498), x being project_in's bf16 output; row_sqnorm's |x - bf16(x)|^2
+    // keeps the prefilter's bound valid for an input that is not bf16-valued.
     const bool x6 = x6_mode(h);
     const int xl = vq_xlayout(h, M);
     const int ntiles = x6 ? dcx::vq_prefilter_ntiles(NC, CD, M, xl) : dcx::vq_argmin_ntiles(NC);
@@ -1744,6 +1778,7 @@ int dcx_create(const dcx_config* cfg, dcx_codec** out) {
   h->compact = !(ncp && ncp[0] == '1');
   const char* vpr = std::getenv("DCX_VQ_PAIRS_PER_ROW");
   if (vpr && vpr[0]) h->vq_pairs_per_row = std::max(0, std::atoi(vpr));
+  knobs_from_env(h->knobs);
   *out = h;
   return DCX_OK;
 }
@@ -2060,7 +2095,9 @@ int dcx_module_io(const dcx_codec* h, const char* module, int32_t* in_channels, 
                   int32_t* out_rate) {
   if (!h || !module) return DCX_ERR_INVALID_ARG;
   int ci = 0, co = 0, r = 1;
-  if (!module_io(h, module, ci, co, r)) return fail(const_cast<dcx_codec*>(h), DCX_ERR_INVALID_ARG, std::string("unknown module: ") + module);
+  // a read-only query: an unknown name returns DCX_ERR_INVALID_ARG without touching the handle's
+  // last-error string (another thread may be running a stage call on the handle)
+  if (!module_io(h, module, ci, co, r)) return DCX_ERR_INVALID_ARG;
   if (in_channels) *in_channels = ci;
   if (out_channels) *out_channels = co;
   if (out_rate) *out_rate = r;
@@ -2120,6 +2157,15 @@ int32_t dcx_get_gemm_mode(const dcx_codec* h) { return h ? h->gemm_mode : -1; }
 int dcx_set_split_k(dcx_codec* h, int32_t max_splits) {
   if (!h || max_splits < 0 || max_splits > kSplitMax) return DCX_ERR_INVALID_ARG;
   h->split_k = max_splits;
+  return DCX_OK;
+}
+
+int dcx_set_knob(dcx_codec* h, const char* name, int32_t value) {
+  if (!h || !name) return DCX_ERR_INVALID_ARG;
+  if (h->busy.load()) return fail(h, DCX_ERR_STATE, "dcx_set_knob during a stage call");
+  int* k = knob_slot(h->knobs, name);
+  if (!k) return fail(h, DCX_ERR_INVALID_ARG, std::string("unknown knob: ") + name);
+  *k = value;
   return DCX_OK;
 }
 

@@ -26,6 +26,7 @@
 // C/D for both: col=l&31, row=(r&3)+8*(r>>2)+4*(l>>5).
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
 
 #include "dcx_kernels.h"
@@ -3739,15 +3740,13 @@ static hipError_t launch_f32(const ConvParams& p, int batch, int phases, hipStre
 template <int BM, int BN, int WM, int WN, int HALO, int PROD, bool AF32>
 static hipError_t launch_x6_persistent(ConvParams p, int batch, int phases, hipStream_t s) {
   auto kern = conv_gemm_x6w8<BM, BN, WM, WN, HALO, false, PROD, AF32>;
-  static int resident = 0;  // workgroups resident per device (per instantiation)
-  if (!resident) {
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WM * WN, 0) != hipSuccess || per_cu < 1)
-      return hipErrorInvalidValue;
-    resident = cus * per_cu;
-  }
+  static std::once_flag once;  // workgroups resident per CU (per instantiation, queried once)
+  static int per_cu = 0;
+  std::call_once(once, [&] {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WM * WN, 0) != hipSuccess) per_cu = 0;
+  });
+  if (per_cu < 1) return hipErrorInvalidValue;
+  const int resident = device_cus() * per_cu;
   p.batch = batch;
   p.phases = phases;
   const long long total = (long long)((p.Lq + BM - 1) / BM) * (p.Cout / BN) * batch * phases;
@@ -3787,32 +3786,33 @@ hipError_t launch_splitk_epilogue(const ConvParams& p, const float* partials, in
 }
 
 // conv_gemm_bf16dp's GELU table: ConvParams::gelu_lut = the table offset from which a wave takes the
-// evaluated epilogue (2 kGeluN, the table's end).  DCX_GELU_LUT (read at each launch): 0 = evaluated
-// always (A/B); a smaller positive limit sends more waves through the evaluated epilogue (tests)
-static int gelu_lut_limit() {
-  const char* e = getenv("DCX_GELU_LUT");
-  if (!e || !*e) return 2 * kGeluN;
-  return std::max(0, std::min(atoi(e), 2 * kGeluN));
+// evaluated epilogue (2 kGeluN, the table's end).  Knobs::gelu_lut (DCX_GELU_LUT at dcx_create): 0 =
+// evaluated always (A/B); a smaller positive limit sends more waves through the evaluated epilogue (tests)
+static int gelu_lut_limit(const Knobs& k) {
+  if (k.gelu_lut < 0) return 2 * kGeluN;
+  return std::min(k.gelu_lut, 2 * kGeluN);
 }
-static bool persist_on() {
-  const char* e = getenv("DCX_BF16_PERSIST");
-  return !(e && e[0] == '0');
+static const Knobs kDefaultKnobs{};
+static const Knobs& knobs(const ConvParams& p) { return p.kn ? *p.kn : kDefaultKnobs; }
+
+// CU count per device, filled once per device (std::call_once per slot; devices past the table are
+// queried each time)
+int device_cus() {
+  constexpr int kDev = 64;
+  static std::once_flag once[kDev];
+  static int cus[kDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  auto query = [dev] {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 8) c = 256;
+    return c;
+  };
+  if (dev < 0 || dev >= kDev) return query();
+  std::call_once(once[dev], [&] { cus[dev] = query(); });
+  return cus[dev];
 }
-static int num_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus < 8)
-      cus = 256;
-  }
-  return cus;
-}
-// DCX_BF16_REG_EPI=0 (read at each launch; A/B and tests): the LDS-staged epilogue for pwconv1 too
-static bool reg_epi_off() {
-  const char* e = getenv("DCX_BF16_REG_EPI");
-  return e && *e == '0';
-}
+static int num_cus() { return device_cus(); }
 
 bool bf16dm_takes(int cin, int cout, int lq, int ldx, int phases) {
 #ifdef DCX_NO_BF16DM
@@ -3875,18 +3875,18 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       ConvParams q = p;
       q.batch = batch;
       q.phases = phases;
-      q.gelu_lut = gelu_lut_limit();
+      q.gelu_lut = gelu_lut_limit(knobs(p));
       const dim3 grid((unsigned)(((p.Lq + 255) / 256) * (p.Cout / 256) * batch * phases));
       // the register epilogue: bias / GELU epilogues with a compact bf16 output only.  With an fp32
       // output too (the VQ blocks' 1x1 convs) or a residual (pwconv2) it measured slower than the
       // staged epilogue, whose 16-byte stores cover 512 contiguous bytes of a row per instruction
       // (C3 bf16dm, A/B: pwconv1 only 52.5 ms, + the fp32-output convs 55.4, + pwconv2 56.6)
       const bool reg = (p.epi == EPI_BIAS || p.epi == EPI_GELU) && p.y6 && p.y_compact == 1 && !p.y && !p.y2 &&
-                       !p.y6s && p.mean_mode == MEAN_NONE && phases == 1 && p.out_mul == 1 && !reg_epi_off();
-      // the persistent form (one step stream across tiles) for compact operands; DCX_BF16_PERSIST=0
-      // (read at each launch) keeps conv_gemm_bf16dm<true> (A/B, same bits)
+                       !p.y6s && p.mean_mode == MEAN_NONE && phases == 1 && p.out_mul == 1 && knobs(p).bf16_reg_epi;
+      // the persistent form (one step stream across tiles) for compact operands; Knobs::bf16_persist = 0
+      // (DCX_BF16_PERSIST=0) keeps conv_gemm_bf16dm<true> (A/B, same bits)
       if (reg && p.x_compact == 1 && p.wc && p.round_bf16 && p.Cin / 32 >= 3 && p.Cout <= kBf16dpBiasMax &&
-          (long long)std::min(256, p.Lq) * p.Cout * 2 < (1ll << 31) && persist_on()) {
+          (long long)std::min(256, p.Lq) * p.Cout * 2 < (1ll << 31) && knobs(p).bf16_persist) {
         if (kname) *kname = "conv_gemm_bf16dp<256,256,reg>";
         const long long tiles = (long long)grid.x;
         const int g = (int)std::min<long long>(num_cus(), (tiles + 7) / 8 * 8);

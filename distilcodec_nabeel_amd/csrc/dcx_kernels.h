@@ -20,6 +20,24 @@ enum Mean : int { MEAN_NONE = 0, MEAN_FIRST = 1, MEAN_MID = 2, MEAN_LAST = 3 };
 
 constexpr int kMaxPhases = 8;
 
+// A/B and test switches.  dcx_create reads them from the environment ONCE into its handle
+// (knobs_from_env, dcx_api.cpp) and dcx_set_knob changes them per handle; no launcher reads the
+// environment, so a captured hipGraph and the eager calls after it run the same kernels.  Every
+// default below is the shipped path.
+struct Knobs {
+  int rp_rows = 0;          // DCX_RP_R: pair-kernel tile height (an instantiated size; 0 = the launcher's choice)
+  int rp_old = 0;           // DCX_RP_OLD=1: the step-schedule pair kernel (conv_res_pair) at C = 32 too
+  int rp_g64 = 0;           // DCX_RP_G64=1: the barrier-free 8-wave pair kernel at C = 64
+  int rp_sync = 0;          // DCX_RP_SYNC=n: a barrier after every n-th tap of conv_res_pair_g
+  int rp_w4 = 0;            // DCX_RP_W4=1: conv_res_pair_w4 (4-wave workgroups, two per CU; A/B)
+  int gelu_lut = -1;        // DCX_GELU_LUT: conv_gemm_bf16dp's table limit (-1 = the whole table, 0 = evaluated)
+  int bf16_persist = 1;     // DCX_BF16_PERSIST=0: the staged bf16dm for pwconv1 instead of bf16dp
+  int bf16_reg_epi = 1;     // DCX_BF16_REG_EPI=0: the LDS-staged epilogue for pwconv1 too
+  int dwconv_tiled = 0;     // DCX_DWCONV_TILED=1: the round-2 tiled dwconv_ln (same bits)
+  int split_min_steps = 0;  // DCX_SPLIT_MIN_STEPS: split-K only convs with at least this many K steps
+  int split_group_off = 0;  // DCX_SPLIT_GROUP_OFF=1: per-conv split launches instead of grouped ones
+};
+
 // out[b][q*out_mul + phase][co] = epi( sum_{m<taps} sum_{ci<Cin} x[b][q + in_base[phase] + m*in_step][ci]
 //                                       * w[phase][co][m*Cin + ci] + bias[co] )
 // Rows of x outside [0, Lin) read as zero (zero padding).  Channels-last everywhere.
@@ -77,8 +95,10 @@ struct ConvParams {
   int diag_skip;
   // conv_gemm_bf16dp with GELU: > 0 = GELU from its LDS table of the bf16 GELU (same bits), a wave
   // with a table offset >= gelu_lut storing the evaluated epilogue instead; 0 = evaluated (set by
-  // launch_conv; DCX_GELU_LUT)
+  // launch_conv from kn)
   int gelu_lut;
+  // the handle's switches (host only; null = the defaults)
+  const Knobs* kn;
 };
 
 // Independent convs issued as one launch (launch_conv_group); problem k owns logical tiles
@@ -124,8 +144,10 @@ struct ResPairParams {
   long long bstride;  // elements between clips
   int L, batch, C;
   // conv_res_pair_g: a workgroup barrier after every tap_sync-th tap of a conv (0: none), which
-  // bounds how far the two waves of a SIMD drift apart before the image hand-offs
+  // bounds how far the two waves of a SIMD drift apart before the image hand-offs (set by
+  // launch_res_pair from kn)
   int tap_sync;
+  const Knobs* kn;  // host only; null = the defaults
 };
 
 // Launchers (all stream-ordered, no allocation).  Return hipError_t of the launch.
@@ -208,7 +230,10 @@ hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, int y6c,
 // bf16: the reference's CUDA autocast (DCX_GEMM_BF16): input, taps and bias rounded to bf16, the
 // depthwise conv's result rounded to bf16, then the fp32 F.layer_norm
 hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6c, const float* dww, const float* dwb,
-                            const float* lnw, const float* lnb, int batch, int L, int C, int bf16, hipStream_t s);
+                            const float* lnw, const float* lnb, int batch, int L, int C, int bf16, const Knobs* kn,
+                            hipStream_t s);
+// the CU count of the current device (cached per device, thread-safe)
+int device_cus();
 // x6 codebook planes -> the per-K32 hi/mid layout of vq_prefilter_bk ((dim / 32) * ncodes * 64 bf16)
 hipError_t launch_repack_codebook_bk(const unsigned short* cb6, int ncodes, int dim, unsigned short* out,
                                      hipStream_t s);

@@ -261,12 +261,13 @@ static void launch_dwconv_ln_nv(const float* x, float* y, unsigned short* y6, in
 }
 
 hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6c, const float* dww, const float* dwb,
-                            const float* lnw, const float* lnb, int batch, int L, int C, int bf16, hipStream_t s) {
-  const char* oe = getenv("DCX_DWCONV_TILED");  // A/B and tests: the round-2 tiled kernel (same bits)
+                            const float* lnw, const float* lnb, int batch, int L, int C, int bf16, const Knobs* kn,
+                            hipStream_t s) {
+  const bool tiled = kn && kn->dwconv_tiled;  // A/B and tests: the round-2 tiled kernel (same bits)
   const long long rows = (long long)batch * L;
   // below 8192 rows (a streaming hop: 93 rows) the tiled kernel's 4-row tiles, one row per wave,
   // measured faster than runs of 1 or 4 rows (C5 hop 4.06-4.09 vs 4.09-4.14 ms, A/B)
-  if (!(oe && *oe && *oe != '0') && rows >= 8192) {
+  if (!tiled && rows >= 8192) {
     // rows per wave: the longest run that still gives >= 2048 waves (8 per CU)
     const int rw = rows >= 2048LL * 32 ? 32 : rows >= 2048LL * 16 ? 16 : rows >= 2048LL * 8 ? 8 : 4;
     if ((long long)batch * ((L + rw - 1) / rw) / 4 >= (1LL << 31)) return hipErrorInvalidValue;

@@ -30,7 +30,6 @@
 // offset, and the weight slot is the global tap slice [chunk][Cout][96 B] copied as is.
 #include <algorithm>
 #include <cstdio>
-#include <cstdlib>
 
 #include "dcx_kernels.h"
 #include "dcx_planes.h"
@@ -685,6 +684,250 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_g(const ResPairParams p)
     for (int i = 0; i < 16; ++i) atomicAdd(&g_rp_diag[(C == 64 ? 16 : 0) + i], dg[i]);
 #endif
 }
+
+// conv_res_pair_w4 (round 5): the barrier-free tap loops of conv_res_pair_g on 4-wave workgroups, TWO
+// per CU.  In the 8-wave kernels the two waves of a SIMD belong to one workgroup and go through the
+// same phases together: both run their tap loops (sharing the matrix pipe, each covering the other's
+// LDS latency only while both are there), then both convert images (VALU only, the matrix pipe idle),
+// then both wait at the hand-off barriers for the slowest wave (PMC: 0.40-0.50 MFMA busy; stamps of
+// the 8-wave barrier-free kernel: taps at 0.92 of MFMA issue for the leading wave, the lagging wave's
+// deficit paid at the next barrier).  Here the partner wave on each SIMD belongs to ANOTHER workgroup,
+// with its own LDS image and barriers, so one workgroup's image conversions, epilogue, S-image loads
+// and barrier waits run beside the other's MFMAs.  Each workgroup owns R output rows of one clip (its
+// image within half the LDS); the S image is filled only over the rows member m's c1 reads (its reach
+// (k - 1) / 2 * d), straight from global memory (the other workgroup covers the load latency).  The
+// MFMAs, their order per accumulator and the layouts are conv_res_pair_g's, so the bits are the same.
+template <int C, int RR>
+struct RpGeom4 {
+  static constexpr int R = RR;
+  static constexpr int M1 = R + 16;               // c1 rows: [r0 - 8, r0 + R + 8)
+  static constexpr int H1 = 32;                   // largest c1 reach
+  static constexpr int NS = M1 + 2 * H1;          // S image rows
+  static constexpr int NCH = C / 16;
+  static constexpr int WC = C / 32, WR = 4 / WC;  // waves: WR row groups x WC column halves
+  static constexpr int NB1 = M1 / 16, RB = NB1 / WR;
+  static constexpr int NB2 = R / 16;
+  static constexpr int BLK = NCH * 1536;
+  static constexpr int IMG = NS / 16 * BLK;
+  static constexpr int G8 = C / 8;
+  static constexpr int WTAP = C * C * 6;
+  static constexpr int FB = 4;                    // S-image items (8 channels) per thread per load batch
+  static constexpr int LDS = IMG + 2 * kMaxGroup * C * 4;
+  static_assert(NB1 % WR == 0 && (NB2 + WR - 1) / WR <= RB, "row blocks per wave");
+  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+};
+template <int C>
+constexpr int kRp4Rows = C == 32 ? 304 : 112;
+
+template <int C, bool MEAN, int RR = kRp4Rows<C>>
+__global__ void __launch_bounds__(256, 2) conv_res_pair_w4(const ResPairParams p) {
+  using G = RpGeom4<C, RR>;
+  constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB, BLK = G::BLK, IMG = G::IMG;
+  constexpr int G8 = G::G8, NS = G::NS, WTAP = G::WTAP, FB = G::FB;
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS];
+  float* const bias_lds = reinterpret_cast<float*>(lds + IMG);  // [conv][member][C]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wc = wave % G::WC, wr = wave / G::WC;
+  const int l15 = lane & 15, hf = (lane >> 4) & 1, t = lane >> 5;
+  const int L = p.L, nmem = p.nmem;
+  const int ntl = (L + R - 1) / R;
+  const int total = ntl * p.batch;
+
+  // ---- S image: silu(state) as planes over the 8-row groups covering [H1 - reach, H1 + M1 + reach)
+  // (zero outside the clip = the conv's padding); rows outside that range are never read ----
+  auto fill = [&](const float* src, int r0, int reach) {
+    const int lo = (G::H1 - reach) & ~7;
+    const int hi = min(NS, (G::H1 + G::M1 + reach + 7) & ~7);
+    const int nit = (hi - lo) * G8;
+    for (int base = 0; base < nit; base += 256 * FB) {
+      f32x4 v[FB][2];
+#pragma unroll
+      for (int k = 0; k < FB; ++k) {  // unconditional loads (index clamped): all in flight at once
+        const int it = min(base + tid + 256 * k, nit - 1);
+        const int s = lo + ((it >> 3) / G8) * 8 + (it & 7), g8 = (it >> 3) % G8;
+        const int a = min(max(r0 - 8 - G::H1 + s, 0), L - 1);
+        const f32x4* q = reinterpret_cast<const f32x4*>(src + (long long)a * C + g8 * 8);
+        v[k][0] = q[0];
+        v[k][1] = q[1];
+      }
+#pragma unroll
+      for (int k = 0; k < FB; ++k) {
+        const int it = base + tid + 256 * k;
+        if (it < nit) {
+          const int s = lo + ((it >> 3) / G8) * 8 + (it & 7), g8 = (it >> 3) % G8;
+          const int a = r0 - 8 - G::H1 + s;
+          const bool ok = a >= 0 && a < L;
+          s16x8 hv, mv, lv;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float sv = rp_silu(v[k][e >> 2][e & 3]);
+            const float x = ok ? sv : 0.f;
+            unsigned short h, m, l;
+            split3(x, h, m, l);
+            hv[e] = (short)h;
+            mv[e] = (short)m;
+            lv[e] = (short)l;
+          }
+          char* d = lds + (s >> 4) * BLK + (g8 >> 1) * 1536 + (g8 & 1) * 768 + (s & 15) * 16;
+          *reinterpret_cast<s16x8*>(d) = hv;
+          *reinterpret_cast<s16x8*>(d + 256) = mv;
+          *reinterpret_cast<s16x8*>(d + 512) = lv;
+        }
+      }
+    }
+  };
+
+  // ---- weight fragments, one tap ahead (conv_res_pair_g) ----
+  s16x8 wf[NCH][2][2];
+  auto load_wf = [&](const unsigned short* wtap, int ch) {
+    const char* wb = reinterpret_cast<const char*>(wtap);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const char* w = wb + (ch * C + (2 * wc + cb) * 16 + l15) * 96 + hf * 48;
+      wf[ch][cb][0] = *reinterpret_cast<const s16x8*>(w + t * 16);
+      wf[ch][cb][1] = *reinterpret_cast<const s16x8*>(w + (t ? 32 : 0));
+    }
+  };
+  auto next_tap = [&](int m, int conv, int j) -> const unsigned short* {
+    if (j + 1 < p.taps[m]) return (conv ? p.w2[m] : p.w1[m]) + (long long)(j + 1) * (WTAP / 2);
+    if (conv == 0) return p.w2[m];
+    return p.w1[m + 1 < nmem ? m + 1 : 0];
+  };
+  const int soX0 = (hf * 3 + t) * 256, soX1 = (hf * 3 + (t ? 0 : 1)) * 256, soX2 = (hf * 3 + (t ? 0 : 2)) * 256;
+  auto tap = [&](f32x4 (&acc)[RB][2], int rowoff, int nrb, const unsigned short* wnext) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        if (i < nrb) {
+          const int sr = (wr + WR * i) * 16 + l15 + rowoff;
+          const char* xr = lds + (sr >> 4) * BLK + (sr & 15) * 16 + ch * 1536;
+          const s16x8 x2 = *reinterpret_cast<const s16x8*>(xr + soX2);
+          const s16x8 x1 = *reinterpret_cast<const s16x8*>(xr + soX1);
+          const s16x8 x0 = *reinterpret_cast<const s16x8*>(xr + soX0);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) {
+            acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][1]),
+                                                                 __builtin_bit_cast(bf16x8, x2), acc[i][cb], 0, 0, 0);
+            acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][0]),
+                                                                 __builtin_bit_cast(bf16x8, x1), acc[i][cb], 0, 0, 0);
+            acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][0]),
+                                                                 __builtin_bit_cast(bf16x8, x0), acc[i][cb], 0, 0, 0);
+          }
+        }
+      }
+      load_wf(wnext, ch);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nrb2 = min(RB, (G::NB2 - wr + WR - 1) / WR);
+  int tile = blockIdx.x;
+  if (tile >= total) return;  // whole workgroup, before any barrier
+  int b = tile / ntl, r0 = (tile - b * ntl) * R;
+  for (int i = tid; i < 2 * nmem * C; i += 256) {
+    const int conv = i / (nmem * C), m = (i / C) % nmem, c = i % C;
+    bias_lds[(conv * kMaxGroup + m) * C + c] = (conv ? p.b2[m] : p.b1[m])[c];
+  }
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) load_wf(p.w1[0], ch);
+  f32x4 macc[MEAN ? RB : 1][2];
+  for (;;) {
+    const int next_tile = tile + gridDim.x;
+    const bool more = next_tile < total;
+    const long long cb0 = (long long)b * p.bstride;
+    for (int m = 0; m < nmem; ++m) {
+      const int k = p.taps[m], hk = (k - 1) >> 1, d = p.dil[m];
+      const bool last_m = m + 1 == nmem;
+      fill(p.src[m] + cb0, r0, hk * d);
+      rp_barrier();
+      // ---- c1 over rows [r0 - 8, r0 + R + 8) from the S image
+      f32x4 acc[RB][2];
+#pragma unroll
+      for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < k; ++j) tap(acc, G::H1 + (j - hk) * d, RB, next_tap(m, 0, j));
+      rp_barrier();  // every wave's S reads are done before T overwrites them
+      // ---- T image: silu(c1 + b1) planes over the S image (zero outside the clip)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(bias_lds + m * C + c0);
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int ir = (wr + WR * i) * 16 + l15, a = r0 - 8 + ir;
+          const bool ok = a >= 0 && a < L;
+          s16x4 hv, mv, lv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float sv = rp_silu(acc[i][cb][e] + bias[e]);
+            const float v = ok ? sv : 0.f;
+            unsigned short h, mm, l;
+            split3(v, h, mm, l);
+            hv[e] = (short)h;
+            mv[e] = (short)mm;
+            lv[e] = (short)l;
+          }
+          char* dst = lds + (ir >> 4) * BLK + (c0 >> 4) * 1536 + ((c0 >> 3) & 1) * 768 + (ir & 15) * 16 + (c0 & 7) * 2;
+          *reinterpret_cast<s16x4*>(dst) = hv;
+          *reinterpret_cast<s16x4*>(dst + 256) = mv;
+          *reinterpret_cast<s16x4*>(dst + 512) = lv;
+        }
+      }
+      rp_barrier();
+      // ---- c2 over rows [r0, r0 + R) from the T image; the residual rows are loaded after tap 0's
+      // fragment reloads
+#pragma unroll
+      for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 res[RB][2];
+      tap(acc, 8 - hk, nrb2, next_tap(m, 1, 0));
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int q = min(r0 + (wr + WR * i) * 16 + l15, L - 1);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+          res[i][cb] = *reinterpret_cast<const f32x4*>(p.src[m] + cb0 + (long long)q * C + c0);
+        }
+      }
+      for (int j = 1; j < k; ++j) tap(acc, 8 + j - hk, nrb2, next_tap(m, 1, j));
+      // ---- epilogue: state + c2 + b2 (rows past the clip end are dropped)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(bias_lds + (kMaxGroup + m) * C + c0);
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          if (i >= nrb2) break;
+          const int q = r0 + (wr + WR * i) * 16 + l15;
+          const f32x4 v = res[i][cb] + (acc[i][cb] + bias);
+          if constexpr (!MEAN) {
+            if (q < L) *reinterpret_cast<f32x4*>(p.dst[m] + cb0 + (long long)q * C + c0) = v;
+          } else if (m == 0) {
+            macc[i][cb] = v;
+          } else if (!last_m) {
+            macc[i][cb] = macc[i][cb] + v;
+          } else {
+            const f32x4 mv = (macc[i][cb] + v) / 3.0f;
+            f32x4 sv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sv[e] = rp_silu(mv[e]);
+            if (q < L) *reinterpret_cast<f32x4*>(p.mean_out + cb0 + (long long)q * C + c0) = sv;
+          }
+        }
+      }
+      rp_barrier();  // every wave's T reads are done before the next S image overwrites them
+    }
+    if (!more) break;
+    tile = next_tile;
+    b = tile / ntl;
+    r0 = (tile - b * ntl) * R;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last tap's (unused) fragment reloads
+}
+
 #ifdef RP_DIAG_STAMPS
 extern "C" int dcx_diag_rp(unsigned long long* out32, int reset) {
   if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_rp_diag), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
@@ -705,74 +948,67 @@ hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** k
         !p.w1[m] || !p.w2[m] || !p.b1[m] || !p.b2[m] || (!p.mean_out && !p.dst[m]))
       return hipErrorInvalidValue;
   }
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus < 1)
-      return hipErrorInvalidValue;
-  }
+  static const Knobs kDefault{};
+  const Knobs& kn = p.kn ? *p.kn : kDefault;
+  const int cus = device_cus();
+  // C = 32: the barrier-free conv_res_pair_g, C = 64: the step schedule; Knobs (A/B and
+  // tests): rp_old runs the step schedule at C = 32 too, rp_g64 the barrier-free kernel at C = 64,
+  // rp_w4 conv_res_pair_w4 (two 4-wave workgroups per CU: same bits, measured 2-6 % slower)
+  const bool w4 = kn.rp_w4 && !kn.rp_old && !kn.rp_g64;
+  const int slots = w4 ? 2 * cus : cus;
   // rows per tile: the default unless a smaller tile finishes the launch sooner, by rounds of tiles
-  // over the CUs times a tile's rows (c1 rows R + 16, c2 rows R, ~64 rows' worth of fixed cost);
-  // DCX_RP_R (read at each launch; tests) forces one of the instantiated sizes
-  static constexpr int kSizes32[3] = {496, 240, 112}, kSizes64[3] = {176, 112, 48};
-  const int* sizes = p.C == 32 ? kSizes32 : kSizes64;
-  int R = sizes[0];
+  // over the workgroup slots times a tile's rows (c1 rows R + 16, c2 rows R, ~64 rows' worth of fixed
+  // cost); Knobs::rp_rows forces one of the instantiated sizes.  Every size gives the same bits.
+  static constexpr int kW8_32[3] = {496, 240, 112}, kW8_64[3] = {176, 112, 48};
+  static constexpr int kW4_32[3] = {304, 112, 48}, kW4_64[3] = {112, 48, 48};
+  const int* sizes = w4 ? (p.C == 32 ? kW4_32 : kW4_64) : (p.C == 32 ? kW8_32 : kW8_64);
+  int si = 0;
   long long best = -1;
   for (int i = 0; i < 3; ++i) {
     const int r = sizes[i];
     const long long tiles = (long long)((p.L + r - 1) / r) * p.batch;
-    const long long cost = (tiles + cus - 1) / cus * (2LL * r + 16 + 64);
+    const long long cost = (tiles + slots - 1) / slots * (2LL * r + 16 + 64);
     if (best < 0 || cost < best) {
       best = cost;
-      R = r;
+      si = i;
     }
   }
-  if (const char* fr = getenv("DCX_RP_R")) {
-    const int r = std::atoi(fr);
-    for (int i = 0; i < 3; ++i)
-      if (sizes[i] == r) R = r;
-  }
+  for (int i = 0; i < 3; ++i)
+    if (kn.rp_rows && sizes[i] == kn.rp_rows) si = i;
+  const int R = sizes[si];
   const long long total = (long long)((p.L + R - 1) / R) * p.batch;
   if (total > (1LL << 30)) return hipErrorInvalidValue;
-  const unsigned grid = (unsigned)std::min<long long>(total, cus);  // one workgroup per CU (LDS)
-  // C = 32: the barrier-free kernel (A/B in one session: 12.4 vs 12.9 ms per C2 generator);
-  // C = 64: the step schedule, which measured faster there (22.3 vs 23.2 ms).
-  // DCX_RP_OLD=1 (read at each launch; A/B and tests) runs the step schedule at C = 32 too.
-  const char* oe = getenv("DCX_RP_OLD");
-  const bool old = oe && *oe && *oe != '0';
-  // A/B switches (read at each launch): DCX_RP_G64=1 runs the barrier-free kernel at C = 64 too,
-  // DCX_RP_SYNC=n puts a barrier after every n-th tap of its conv loops
-  const char* g64 = getenv("DCX_RP_G64");
-  const char* sy = getenv("DCX_RP_SYNC");
+  const unsigned grid = (unsigned)std::min<long long>(total, slots);  // resident workgroups (LDS)
   ResPairParams q = p;
-  q.tap_sync = sy && *sy ? std::max(0, std::atoi(sy)) : 0;
-  static char names[64];
-  auto launch = [&](auto kern, const char* base, const ResPairParams& a) {
-    if (kname) {
-      snprintf(names, sizeof names, "%s%s%s", base, p.mean_out ? ",mean" : "", R == sizes[0] ? ">" : ",small>");
-      *kname = names;
-    }
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, s, a);
-  };
-#define DCX_RP_LAUNCH(KERN, CC, A)                                                                       \
-  do {                                                                                                   \
-    const char* base_ = #KERN "<" #CC;                                                                   \
-    if (R == sizes[0]) {                                                                                 \
-      if (p.mean_out) launch(KERN<CC, true>, base_, A); else launch(KERN<CC, false>, base_, A);          \
-    } else if (R == sizes[1]) {                                                                          \
-      if (p.mean_out) launch(KERN<CC, true, (CC == 32 ? 240 : 112)>, base_, A);                          \
-      else launch(KERN<CC, false, (CC == 32 ? 240 : 112)>, base_, A);                                    \
-    } else {                                                                                             \
-      if (p.mean_out) launch(KERN<CC, true, (CC == 32 ? 112 : 48)>, base_, A);                           \
-      else launch(KERN<CC, false, (CC == 32 ? 112 : 48)>, base_, A);                                     \
-    }                                                                                                    \
+  q.tap_sync = std::max(0, kn.rp_sync);
+  const bool mean = p.mean_out != nullptr;
+  // profile names are string literals (no shared buffer between threads)
+#define DCX_RP_GO(KERN, CC, RR, NAME)                                                       \
+  do {                                                                                      \
+    if (kname) *kname = mean ? #KERN "<" #CC ",mean" NAME ">" : #KERN "<" #CC NAME ">";     \
+    if (mean) hipLaunchKernelGGL((KERN<CC, true, RR>), dim3(grid), dim3(w4 ? 256 : 512), 0, s, q);   \
+    else hipLaunchKernelGGL((KERN<CC, false, RR>), dim3(grid), dim3(w4 ? 256 : 512), 0, s, q);       \
   } while (0)
-  if (p.C == 32 && !old) DCX_RP_LAUNCH(conv_res_pair_g, 32, q);
-  else if (p.C == 64 && !old && g64 && *g64 == '1') DCX_RP_LAUNCH(conv_res_pair_g, 64, q);
-  else if (p.C == 32) DCX_RP_LAUNCH(conv_res_pair, 32, p);
-  else DCX_RP_LAUNCH(conv_res_pair, 64, p);
-#undef DCX_RP_LAUNCH
+#define DCX_RP_SIZES(KERN, CC, R0, R1, R2)                     \
+  do {                                                         \
+    if (si == 0) DCX_RP_GO(KERN, CC, R0, "");                  \
+    else if (si == 1) DCX_RP_GO(KERN, CC, R1, ",small");       \
+    else DCX_RP_GO(KERN, CC, R2, ",small");                    \
+  } while (0)
+  if (w4) {
+    if (p.C == 32) DCX_RP_SIZES(conv_res_pair_w4, 32, 304, 112, 48);
+    else DCX_RP_SIZES(conv_res_pair_w4, 64, 112, 48, 48);
+  } else if (p.C == 32 && !kn.rp_old) {
+    DCX_RP_SIZES(conv_res_pair_g, 32, 496, 240, 112);
+  } else if (p.C == 64 && !kn.rp_old && kn.rp_g64) {
+    DCX_RP_SIZES(conv_res_pair_g, 64, 176, 112, 48);
+  } else if (p.C == 32) {
+    DCX_RP_SIZES(conv_res_pair, 32, 496, 240, 112);
+  } else {
+    DCX_RP_SIZES(conv_res_pair, 64, 176, 112, 48);
+  }
+#undef DCX_RP_SIZES
+#undef DCX_RP_GO
   return hipGetLastError();
 }
 

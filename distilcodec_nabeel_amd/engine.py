@@ -5,6 +5,7 @@ pointers to the C ABI.  Tensors are channels-last ([B][T][C]) as the kernels pro
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -18,6 +19,13 @@ from .config import check_supported
 # codebook EMA statistics a trained checkpoint carries (vector_quantize_pytorch.py:508-531); eval
 # never reads them, and embed_avg alone is as large as the codebook (470 MB), so they are not copied
 _TRAINING_ONLY = ("_codebook.embed_avg", "_codebook.cluster_size")
+
+# dcx_set_knob switches and their shipped values (include/distilcodec_amd.h; dcx::Knobs)
+KNOB_DEFAULTS = {
+    "DCX_RP_R": 0, "DCX_RP_OLD": 0, "DCX_RP_G64": 0, "DCX_RP_SYNC": 0, "DCX_RP_W4": 0, "DCX_GELU_LUT": -1,
+    "DCX_BF16_PERSIST": 1, "DCX_BF16_REG_EPI": 1, "DCX_DWCONV_TILED": 0, "DCX_SPLIT_MIN_STEPS": 0,
+    "DCX_SPLIT_GROUP_OFF": 0,
+}
 
 GEMM_MODES = {"f32": _native.DCX_GEMM_F32, "x6": _native.DCX_GEMM_X6, "bf16": _native.DCX_GEMM_BF16}
 
@@ -126,6 +134,23 @@ class NativeCodec:
         Opt-in for small batches; results then depend on the tile count (not batch-invariant)."""
         self._check(self.L.dcx_set_split_k(self.h, int(max_splits)))
         self._ws = None  # the workspace size changed
+
+    def set_knob(self, name: str, value: int) -> None:
+        """A/B and test switch of the kernel selection (dcx_set_knob; names are the DCX_* environment
+        variables dcx_create reads once).  Takes effect for later calls on this engine."""
+        self._check(self.L.dcx_set_knob(self.h, name.encode(), int(value)))
+
+    @contextlib.contextmanager
+    def knobs(self, **values):
+        """Switches set for the calls inside the block, then back to the shipped defaults
+        (KNOB_DEFAULTS): `with eng.knobs(DCX_RP_OLD=1): ...`."""
+        for k, v in values.items():
+            self.set_knob(k, v)
+        try:
+            yield self
+        finally:
+            for k in values:
+                self.set_knob(k, KNOB_DEFAULTS[k])
 
     def num_frames(self, n_samples: int) -> int:
         return int(self.L.dcx_num_frames(self.h, n_samples))

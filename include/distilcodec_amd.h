@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define DCX_ABI_VERSION 2
+#define DCX_ABI_VERSION 3
 
 enum {
   DCX_OK = 0,
@@ -191,6 +191,15 @@ int32_t dcx_get_gemm_mode(const dcx_codec* h);
  * clip inside a batch; fp32-level differences).  Takes effect for later calls; size workspaces after. */
 int dcx_set_split_k(dcx_codec* h, int32_t max_splits);
 
+/* A/B and test switches of the kernel selection (no reference counterpart).  dcx_create reads them
+ * ONCE from the environment variables of the same names (DCX_RP_R, DCX_RP_OLD, DCX_RP_G64,
+ * DCX_RP_SYNC, DCX_RP_W4, DCX_GELU_LUT, DCX_BF16_PERSIST, DCX_BF16_REG_EPI, DCX_DWCONV_TILED,
+ * DCX_SPLIT_MIN_STEPS, DCX_SPLIT_GROUP_OFF); no launch reads the environment.  This call changes
+ * one for later calls on this handle (a hipGraph captured earlier keeps the kernels it captured).
+ * Unset, every switch selects the shipped path.  DCX_ERR_INVALID_ARG for an unknown name,
+ * DCX_ERR_STATE during a stage call. */
+int dcx_set_knob(dcx_codec* h, const char* name, int32_t value);
+
 /* Standalone 1-D convolution primitive (the kernel family behind every stage), for tests and
  * benchmarks.  weight: host fp32, Conv1d layout [Cout][Cin][k] (transposed=0) or
  * ConvTranspose1d layout [Cin][Cout][k] (transposed=1, padding (k-stride)/2); bias may be NULL.
@@ -228,7 +237,8 @@ void dcx_conv_destroy(dcx_conv* c);
  *   "generator.conv_post": the generator's tail, SiLU -> conv_post -> tanh (generators.py:141-145),
  *       y [B][rows][1];
  *   "quantizer.search": nearest code (vector_quantize_pytorch.py:41-45, 496-506) of x_pjt_in rows
- *       x [B][rows][codebook_dim]; y = int32 codes [B][rows] (x6 and fp32 modes).
+ *       x [B][rows][codebook_dim]; y = int32 codes [B][rows] (every mode: the exact nearest code of x
+ *       as given; in bf16 mode through the pipeline's compact-operand prefilter).
  * dcx_module_io reports a module's input channels, output channels (0: int32 codes) and output rows
  * per input row; unknown names return DCX_ERR_INVALID_ARG (and dcx_module_workspace_size 0).
  * dcx_module_forward takes the input's channel count and returns DCX_ERR_INVALID_ARG unless it is the

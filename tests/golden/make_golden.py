@@ -288,9 +288,8 @@ def make_bf16(codec, audio_batch):
         wav_wn = codec.generator(codec.quantizer.decode(a["codes"]))[:, 0]
     _store(d, "wav_wn64", wav_wn)
     d["wn64_dist_wav"] = np.float64(_rel(wav_wn, a["wav"]))
-    for k in ("feat", "x_pjt_in", "wav"):
-        if k != "wav":  # the decode is stored with the fp64 weight-norm fold (wav_wn64)
-            _store(d, k, a[k])
+    for k in ("feat", "x_pjt_in", "wav"):  # the decode also with the fp64 weight-norm fold (wav_wn64)
+        _store(d, k, a[k])
         d[f"spread_{k}"] = np.float64(_rel(b[k], a[k]))
     d["spread_wav_same_codes"] = np.float64(_rel(wav1, a["wav"]))
     d["codes"] = _np(a["codes"][0, :, :, 0]).astype(np.int64)
@@ -320,11 +319,10 @@ def make_bf16(codec, audio_batch):
                 if name.startswith("generator.resblocks.") and name.count(".") == 2:
                     yf = torch.nn.functional.silu(yf)
         _store(d, f"m:{name}:in", x)
-        if name.startswith("generator."):  # weight-normed convs: the output with the library's fp64 fold
+        _store(d, f"m:{name}:out", y)
+        if name.startswith("generator."):  # weight-normed convs: also the output with the library's fp64 fold
             _store(d, f"m:{name}:out_wn64", yw)
             d[f"m:{name}:wn64_dist"] = np.float64(_rel(yw, y))
-        else:
-            _store(d, f"m:{name}:out", y)
         d[f"m:{name}:spread"] = np.float64(_rel(y1, y))
         d[f"m:{name}:exact_spread"] = np.float64(_rel(ye, y))
         d[f"m:{name}:fp32_dist"] = np.float64(_rel(yf, y))

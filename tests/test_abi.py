@@ -28,7 +28,7 @@ def test_header_symbols_exported_and_bound():
         assert hasattr(L, n), n
         assert n in _native.SIGNATURES, f"{n} has no ctypes signature"
     assert set(_native.SIGNATURES) == set(names)
-    assert L.dcx_abi_version() == 2
+    assert L.dcx_abi_version() == 3
 
 
 def test_config_struct_matches_default(cfg):
@@ -96,3 +96,38 @@ def test_engine_refuses_cpu(cfg, state):
 
     with pytest.raises(_native.NativeUnavailable):
         NativeCodec(cfg, state, "cpu")
+
+
+def test_knobs_are_per_handle(cfg, monkeypatch):
+    """A/B switches are read from the environment once, at dcx_create, and changed per handle by
+    dcx_set_knob (round 5: no launcher reads the environment); unknown names are rejected."""
+    from distilcodec_nabeel_amd import _native
+    from distilcodec_nabeel_amd.engine import KNOB_DEFAULTS
+
+    L = _native.lib()
+    c = _native.config_from_dict(cfg)
+    h = ctypes.c_void_p()
+    assert L.dcx_create(ctypes.byref(c), ctypes.byref(h)) == 0
+    try:
+        for name, v in KNOB_DEFAULTS.items():
+            assert L.dcx_set_knob(h, name.encode(), v) == 0, name
+        assert L.dcx_set_knob(h, b"DCX_RP_OLD", 1) == 0
+        assert L.dcx_set_knob(h, b"DCX_NOT_A_KNOB", 1) == _native.DCX_ERR_INVALID_ARG
+        assert b"unknown knob" in L.dcx_last_error(h)
+        assert L.dcx_set_knob(None, b"DCX_RP_OLD", 1) == _native.DCX_ERR_INVALID_ARG
+    finally:
+        L.dcx_destroy(h)
+    # a handle created with a knob in the environment: still settable, and unknown module names are
+    # rejected by the read-only dcx_module_io without writing the handle's error text
+    monkeypatch.setenv("DCX_RP_W4", "1")
+    h = ctypes.c_void_p()
+    assert L.dcx_create(ctypes.byref(c), ctypes.byref(h)) == 0
+    try:
+        assert L.dcx_set_knob(h, b"DCX_RP_W4", 0) == 0
+        before = L.dcx_last_error(h)
+        ci, co, r = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        assert L.dcx_module_io(h, b"no.such.module", ctypes.byref(ci), ctypes.byref(co), ctypes.byref(r)) == \
+            _native.DCX_ERR_INVALID_ARG
+        assert L.dcx_last_error(h) == before
+    finally:
+        L.dcx_destroy(h)

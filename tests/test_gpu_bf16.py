@@ -99,7 +99,7 @@ def test_decode_bf16(beng, golden, name):
     ref = np.asarray(g["wav"], np.float64)
     snr = 10 * np.log10((ref ** 2).sum() / ((wav - ref) ** 2).sum())
     print(f"\nbf16 decode vs fp32 reference: snr {snr:.2f} dB")
-    assert snr >= 30
+    assert snr >= 35  # measured 39.2-39.7 dB; the reference's own bf16 decode: 39.2 dB
 
 
 @pytest.fixture(scope="module")
@@ -158,9 +158,8 @@ def test_compact_layout_same_bits(beng, cfg, state, B, secs):
 def test_register_epilogue_same_bits(beng):
     """conv_gemm_bf16dm's register epilogue for the pwconv1 launches (MFMA operands swapped, bias +
     GELU + compact stores from the accumulators) against the LDS-staged epilogue
-    (DCX_BF16_REG_EPI=0, read at each launch): encoder features, x_pjt_in and codes bit for bit on a
+    (DCX_BF16_REG_EPI=0 through dcx_set_knob): encoder features, x_pjt_in and codes bit for bit on a
     batch that puts every 1x1 conv on conv_gemm_bf16dm (4 x 11 s)."""
-    import os
 
     from distilcodec_nabeel_amd import synth
 
@@ -170,14 +169,11 @@ def test_register_epilogue_same_bits(beng):
         audio[i, 1:] = torch.from_numpy(c)
     audio = audio.cuda()
     outs = []
-    for flag in ("1", "0"):
-        os.environ["DCX_BF16_REG_EPI"] = flag
-        try:
+    for flag in (1, 0):
+        with beng.knobs(DCX_BF16_REG_EPI=flag):
             feat = beng.encode(beng.mel(audio))
             codes, pin, _, q = beng.vq_encode(feat, want_fup=False)
             torch.cuda.synchronize()
-        finally:
-            del os.environ["DCX_BF16_REG_EPI"]
         outs.append((feat.clone(), codes.clone(), pin.clone(), q.clone()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
@@ -189,7 +185,6 @@ def test_persistent_same_bits(beng):
     bit, with the table (default), with table limits that send waves with a pre-GELU |x| >= 4
     (DCX_GELU_LUT=8448, a few) or >= 1 (7936, nearly all) through the evaluated epilogue over the
     table's stores, and evaluated throughout (DCX_GELU_LUT=0).  4 x 11 s clips, every 1x1 conv on the bf16 kernels."""
-    import os
 
     from distilcodec_nabeel_amd import synth
 
@@ -199,16 +194,11 @@ def test_persistent_same_bits(beng):
         audio[i, 1:] = torch.from_numpy(c)
     audio = audio.cuda()
     outs = []
-    for env in ({"DCX_BF16_PERSIST": "0"}, {}, {"DCX_GELU_LUT": "8448"}, {"DCX_GELU_LUT": "7936"},
-                {"DCX_GELU_LUT": "0"}):
-        os.environ.update(env)
-        try:
+    for kn in ({"DCX_BF16_PERSIST": 0}, {}, {"DCX_GELU_LUT": 8448}, {"DCX_GELU_LUT": 7936}, {"DCX_GELU_LUT": 0}):
+        with beng.knobs(**kn):
             feat = beng.encode(beng.mel(audio))
             codes, pin, _, q = beng.vq_encode(feat, want_fup=False)
             torch.cuda.synchronize()
-        finally:
-            for k in env:
-                del os.environ[k]
         outs.append((feat.clone(), codes.clone(), pin.clone(), q.clone()))
     for o in outs[1:]:
         for a, b in zip(outs[0], o):

@@ -163,10 +163,9 @@ def test_unknown_module_raises(eng):
 @pytest.mark.parametrize("B,secs", [(10, 10.0), (24, 10.0), (72, 10.0)])
 def test_dwconv_run_same_bits_as_tiled(cfg, state, gemm, B, secs):
     """dwconv_ln_run (one wave per run of rows, register window; launches of >= 8192 rows) against
-    the round-2 tiled kernel (DCX_DWCONV_TILED=1, read at each launch): the same per-row arithmetic,
+    the round-2 tiled kernel (DCX_DWCONV_TILED=1 through dcx_set_knob): the same per-row arithmetic,
     so the encoder features are bit-identical, for runs of 4 (10 x 10 s: 9370 rows), 8 (24 x 10 s)
     and 32 rows (72 x 10 s: 67464 rows), in the x6 and bf16 modes (fp32 / planes / compact outputs)."""
-    import os
 
     from distilcodec_nabeel_amd import synth
     from distilcodec_nabeel_amd.engine import NativeCodec
@@ -179,12 +178,9 @@ def test_dwconv_run_same_bits_as_tiled(cfg, state, gemm, B, secs):
         audio[i, 1:] = torch.from_numpy(c)
     mel = e.mel(audio.cuda())
     a = e.encode(mel).clone()
-    os.environ["DCX_DWCONV_TILED"] = "1"
-    try:
+    with e.knobs(DCX_DWCONV_TILED=1):
         b = e.encode(mel)
         torch.cuda.synchronize()
-    finally:
-        del os.environ["DCX_DWCONV_TILED"]
     assert torch.isfinite(a).all()
     assert torch.equal(a, b)
 

@@ -79,42 +79,40 @@ def test_fused_batch_invariance(engines):
 
 
 @pytest.mark.parametrize("B,T", [(1, 1), (2, 7), (3, 40), (8, 200)])
-def test_unit_pipeline_same_bits_as_step_schedule(engines, B, T):
-    """conv_res_pair_g (barrier-free tap loops, fragments loaded from L2 a tap ahead; the C = 32 stage) against the round-2 step
-    schedule (DCX_RP_OLD=1, read at each launch): the same MFMAs in the same order, so the same bits,
-    also over many tiles per workgroup (B=8, T=200: the persistent tile loop and the ring's
-    wrap-around past the last tile)."""
+def test_pair_kernels_same_bits(engines, B, T):
+    """The shipped pair kernels (the barrier-free conv_res_pair_g at C = 32, the step schedule
+    conv_res_pair at C = 64) against conv_res_pair_w4 (DCX_RP_W4=1: 4-wave workgroups, two per CU), the
+    step schedule at both (DCX_RP_OLD=1) and the barrier-free kernel at both (DCX_RP_G64=1), switched
+    per engine with dcx_set_knob: the same MFMAs in the same order per
+    accumulator, so the same bits, also over many tiles per workgroup (B=8, T=200: the persistent tile
+    loop and the weight stream's wrap-around past the last tile)."""
     fused, _ = engines
     z = _z(B, T, 300 + T)
     a = fused.generate(z)
-    os.environ["DCX_RP_OLD"] = "1"
-    try:
-        b = fused.generate(z)
-    finally:
-        del os.environ["DCX_RP_OLD"]
+    outs = []
+    for kn in ({"DCX_RP_W4": 1}, {"DCX_RP_OLD": 1}, {"DCX_RP_G64": 1}):
+        with fused.knobs(**kn):
+            outs.append(fused.generate(z))
     torch.cuda.synchronize()
     assert torch.isfinite(a).all()
-    assert torch.equal(a, b)
+    for b in outs:
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("B,T", [(1, 93), (2, 31), (1, 7)])
 def test_tile_rows_same_bits(engines, B, T):
-    """The pair kernels on smaller tiles (round 4: 240 / 112 rows at C = 32, 112 / 48 at C = 64, which
-    the launcher takes when the default 496 / 176 leave most CUs idle, e.g. the C5 hop): every
-    output row is computed with the same arithmetic whatever the tile, so every size (DCX_RP_R, read
-    at each launch) gives the same bits as the default on both the step-schedule and the
-    barrier-free kernels."""
+    """The pair kernels on every tile height they are instantiated for (conv_res_pair_w4: 304 / 112 / 48
+    rows at C = 32, 112 / 48 at C = 64; the 8-wave kernels: 496 / 240 / 112 at C = 32, 176 / 112 / 48
+    at C = 64), which the launcher picks by tile rounds (smaller ones for the C5 hop): every output
+    row is computed with the same arithmetic whatever the tile, so every size (DCX_RP_R) gives the
+    same bits as the default, on the w4, step-schedule and barrier-free kernels."""
     fused, _ = engines
     z = _z(B, T, 500 + T)
     outs = []
-    for r in ("496", "240", "112", "176", "48"):
-        for old in ("0", "1"):
-            os.environ["DCX_RP_R"] = r
-            os.environ["DCX_RP_OLD"] = old
-            try:
+    for r in (304, 496, 240, 112, 176, 48):
+        for kn in ({}, {"DCX_RP_W4": 1}, {"DCX_RP_OLD": 1}):
+            with fused.knobs(DCX_RP_R=r, **kn):
                 outs.append(fused.generate(z))
-            finally:
-                del os.environ["DCX_RP_R"], os.environ["DCX_RP_OLD"]
     torch.cuda.synchronize()
     assert torch.isfinite(outs[0]).all()
     for o in outs[1:]:

@@ -88,9 +88,8 @@ def test_graph_hop_on_split_engine(engines):
 def test_grouped_split_launches(engines, cfg, state, T):
     """The three ResBlocks' convs of one dilation index as one grouped split-K launch plus one
     grouped reduce (round 4): the grouped kernel runs (profile), the generator output is within the
-    fp32 summation-order distance of the per-conv split launches (DCX_SPLIT_GROUP_OFF=1, read at
-    each call) and of the fp64 oracle (>= 80 dB)."""
-    import os
+    fp32 summation-order distance of the per-conv split launches (DCX_SPLIT_GROUP_OFF=1 through
+    dcx_set_knob) and of the fp64 oracle (>= 80 dB)."""
 
     from oracle import reference_cpu as R
 
@@ -103,13 +102,34 @@ def test_grouped_split_launches(engines, cfg, state, T):
     names = split.profile_read()
     split.profile(False)
     assert any("x6pp_group" in k for k in names), sorted(names)
-    os.environ["DCX_SPLIT_GROUP_OFF"] = "1"
-    try:
+    with split.knobs(DCX_SPLIT_GROUP_OFF=1):
         wav_single = split.generate(z).cpu().reshape(-1)
-    finally:
-        del os.environ["DCX_SPLIT_GROUP_OFF"]
     with torch.no_grad():
         ref = R.generator(z.transpose(1, 2).double(), state["generator"], cfg["decoder"], torch.float64).reshape(-1)
     s1, s2 = _snr(wav, ref), _snr(wav, wav_single)
     print(f"T={T}: grouped split-K vs fp64 oracle {s1:.1f} dB, vs per-conv split {s2:.1f} dB")
     assert s1 >= 80 and s2 >= 100
+
+
+def test_grouped_split_respects_split_k(cfg, state):
+    """dcx_set_split_k(2) caps the grouped split launches too (round-4 ADVICE: they allocated up to 16
+    K-slices per member whatever the handle's limit).  With at most 2 slices per member the grouped and
+    the per-conv split launches (DCX_SPLIT_GROUP_OFF=1) give every conv 2 slices, the same partial sums
+    and the same reduce order: the same bits.  A grouped launch that ignored the cap would not."""
+    from distilcodec_nabeel_amd.engine import NativeCodec
+
+    e = NativeCodec(cfg, state, "cuda:0", gemm="x6")
+    e.set_split_k(2)
+    g = torch.Generator().manual_seed(77)
+    z = torch.randn(1, 93, 1024, generator=g) * 0.5
+    e.profile(True)
+    e.profile_reset()
+    wav = e.generate(z)
+    names = e.profile_read()
+    e.profile(False)
+    assert any("x6pp_group" in k for k in names), sorted(names)
+    with e.knobs(DCX_SPLIT_GROUP_OFF=1):
+        wav_single = e.generate(z)
+    torch.cuda.synchronize()
+    assert torch.isfinite(wav).all()
+    assert torch.equal(wav, wav_single)
