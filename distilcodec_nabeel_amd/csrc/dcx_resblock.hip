@@ -25,9 +25,11 @@
 //   W{h',m'} . X{h,m} = hh' + mm',  W{h',m'} . X{m,h} = mh' + hm',  W{h',l'} . X{l,h} = lh' + hl'.
 // Weights stream through a 2-slot LDS ring, one tap (C * C * 6 bytes) per step, prefetched one
 // step ahead into registers; the step sequence runs on across convs, ResBlocks and tiles.
-// LDS images: 16-row blocks, [row >> 4][chunk][piece 6][row & 15][16 B] (piece = half * 3 +
-// plane), so every ds_read_b128 of 16 consecutive rows of one piece is conflict-free at any tap
-// offset, and the weight slot is the global tap slice [chunk][Cout][96 B] copied as is.
+// LDS images: piece-major and row-linear, byte ((chunk * 6 + piece) * NS + row) * 16 (piece = half * 3 +
+// plane, NS the image rows, a multiple of 16): every ds_read_b128 of 16 consecutive rows of one piece
+// is conflict-free at any tap offset, and a tap's row offset is one add per read set (round 5; the
+// round-2 layout of 16-row blocks cost ~6 VALU per row block and tap in address arithmetic).  The
+// weight slot is the global tap slice [chunk][Cout][96 B] copied as is.
 #include <algorithm>
 #include <cstdio>
 
@@ -84,8 +86,8 @@ struct RpGeom {
   static constexpr int WC = C / 32, WR = 8 / WC; // waves: WR row groups x WC column halves (32 ch)
   static constexpr int NB1 = M1 / 16, RB1 = NB1 / WR;
   static constexpr int NB2 = R / 16, RB2 = (NB2 + WR - 1) / WR;
-  static constexpr int BLK = NCH * 1536;         // bytes per 16-row block of an image
-  static constexpr int IMG = NS / 16 * BLK;      // S image bytes (T reuses its start)
+  static constexpr int PS = NS * 16;             // bytes per piece of one chunk (image layout below)
+  static constexpr int IMG = NCH * 6 * PS;       // S image bytes (T reuses its start)
   static constexpr int TPS = C == 32 ? 2 : 1;    // taps per step (weight slot)
   static constexpr int WTAP = C * C * 6;         // one tap of weights
   static constexpr int WSLOT = TPS * WTAP;
@@ -102,7 +104,7 @@ struct RpGeom {
 template <int C, bool MEAN, int RR = kRpRows<C>>
 __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
   using G = RpGeom<C, RR>;
-  constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB1, BLK = G::BLK, IMG = G::IMG, TPS = G::TPS;
+  constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB1, PS = G::PS, IMG = G::IMG, TPS = G::TPS;
   constexpr int WTAP = G::WTAP, WSLOT = G::WSLOT, G8 = G::G8, NIT = G::NIT, WP = G::WP, WPW = G::WPW, NS = G::NS;
   __shared__ __attribute__((aligned(16))) char lds[G::LDS];
   float* const bias_lds = reinterpret_cast<float*>(lds + IMG + 2 * WSLOT);  // [conv][member][C]
@@ -163,16 +165,19 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
         mv[e] = (short)m;
         lv[e] = (short)l;
       }
-      char* d = lds + (s >> 4) * BLK + (g8 >> 1) * 1536 + (g8 & 1) * 768 + (s & 15) * 16;
+      char* d = lds + ((g8 >> 1) * 6 + (g8 & 1) * 3) * PS + s * 16;
       *reinterpret_cast<s16x8*>(d) = hv;
-      *reinterpret_cast<s16x8*>(d + 256) = mv;
-      *reinterpret_cast<s16x8*>(d + 512) = lv;
+      *reinterpret_cast<s16x8*>(d + PS) = mv;
+      *reinterpret_cast<s16x8*>(d + 2 * PS) = lv;
     }
   };
 
   // ---- one step: the step's taps, every chunk, rows of this wave, its 2 column blocks.  hook(i)
   // runs after row block i of the first tap (global loads spread between the MFMAs) ----
-  const int soX0 = (hf * 3 + t) * 256, soX1 = (hf * 3 + (t ? 0 : 1)) * 256, soX2 = (hf * 3 + (t ? 0 : 2)) * 256;
+  // lane parts of the three activation reads (piece, row within the 16-row block); a tap adds its
+  // wave-uniform row offset once, and row block / chunk offsets are instruction immediates
+  const int pk0 = ((hf * 3 + t) * NS + l15) * 16, pk1 = ((hf * 3 + (t ? 0 : 1)) * NS + l15) * 16;
+  const int pk2 = ((hf * 3 + (t ? 0 : 2)) * NS + l15) * 16;
   auto mfma_step = [&](f32x4 (&acc)[RB][2], int slot, int ntaps, int row0, int rstep, int nrb, auto hook) {
 #pragma unroll
     for (int u = 0; u < TPS; ++u) {
@@ -188,17 +193,18 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
           wf[ch][cb][1] = *reinterpret_cast<const s16x8*>(w + (t ? 32 : 0));  // {h', l'}
         }
       const int rowoff = row0 + u * rstep;
+      const int tb = (wr * 16 + rowoff) * 16;
+      const char *xb0 = lds + pk0 + tb, *xb1 = lds + pk1 + tb, *xb2 = lds + pk2 + tb;
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
         if (i < nrb) {
-          const int sr = (wr + WR * i) * 16 + l15 + rowoff;
-          const char* xr = lds + (sr >> 4) * BLK + (sr & 15) * 16;
+          const int io = (WR * 16 * i) * 16;
 #pragma unroll
           for (int ch = 0; ch < NCH; ++ch) {
-            const s16x8 x2 = *reinterpret_cast<const s16x8*>(xr + ch * 1536 + soX2);
-            const s16x8 x1 = *reinterpret_cast<const s16x8*>(xr + ch * 1536 + soX1);
-            const s16x8 x0 = *reinterpret_cast<const s16x8*>(xr + ch * 1536 + soX0);
+            const s16x8 x2 = *reinterpret_cast<const s16x8*>(xb2 + io + ch * 6 * PS);
+            const s16x8 x1 = *reinterpret_cast<const s16x8*>(xb1 + io + ch * 6 * PS);
+            const s16x8 x0 = *reinterpret_cast<const s16x8*>(xb0 + io + ch * 6 * PS);
 #pragma unroll
             for (int cb = 0; cb < 2; ++cb) {
               acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][1]),
@@ -293,10 +299,10 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
             mv[e] = (short)mm;
             lv[e] = (short)l;
           }
-          char* dst = lds + (ir >> 4) * BLK + (c0 >> 4) * 1536 + ((c0 >> 3) & 1) * 768 + (ir & 15) * 16 + (c0 & 7) * 2;
+          char* dst = lds + ((c0 >> 4) * 6 + ((c0 >> 3) & 1) * 3) * PS + ir * 16 + (c0 & 7) * 2;
           *reinterpret_cast<s16x4*>(dst) = hv;
-          *reinterpret_cast<s16x4*>(dst + 256) = mv;
-          *reinterpret_cast<s16x4*>(dst + 512) = lv;
+          *reinterpret_cast<s16x4*>(dst + PS) = mv;
+          *reinterpret_cast<s16x4*>(dst + 2 * PS) = lv;
         }
       }
       rp_barrier();
@@ -421,7 +427,7 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair(const ResPairParams p) {
 template <int C, bool MEAN, int RR = kRpRows<C>>
 __global__ void __launch_bounds__(512, 1) conv_res_pair_g(const ResPairParams p) {
   using G = RpGeom<C, RR>;
-  constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB1, BLK = G::BLK, IMG = G::IMG;
+  constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB1, PS = G::PS, IMG = G::IMG;
   constexpr int G8 = G::G8, NIT = G::NIT, NS = G::NS, WTAP = G::WTAP;
   __shared__ __attribute__((aligned(16))) char lds[IMG + 2 * kMaxGroup * C * 4];
   float* const bias_lds = reinterpret_cast<float*>(lds + IMG);  // [conv][member][C]
@@ -462,23 +468,26 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_g(const ResPairParams p)
         mv[e] = (short)m;
         lv[e] = (short)l;
       }
-      char* d = lds + (s >> 4) * BLK + (g8 >> 1) * 1536 + (g8 & 1) * 768 + (s & 15) * 16;
+      char* d = lds + ((g8 >> 1) * 6 + (g8 & 1) * 3) * PS + s * 16;
       *reinterpret_cast<s16x8*>(d) = hv;
-      *reinterpret_cast<s16x8*>(d + 256) = mv;
-      *reinterpret_cast<s16x8*>(d + 512) = lv;
+      *reinterpret_cast<s16x8*>(d + PS) = mv;
+      *reinterpret_cast<s16x8*>(d + 2 * PS) = lv;
     }
   };
 
   // ---- weight fragments of chunk ch of a tap ([chunk][Cout][96 B], the ConvParams::w6 tap slice):
   // [column block][{h',m'} | {h',l'}] ----
   s16x8 wf[NCH][2][2];
+  // buffer loads: the lane offsets are loop-invariant VGPRs, the tap base a scalar resource and the
+  // chunk / column-block offsets scalar constants, so a reload costs no address arithmetic
+  const int wo0 = ((2 * wc) * 16 + l15) * 96 + hf * 48 + t * 16, wo1 = ((2 * wc) * 16 + l15) * 96 + hf * 48 + (t ? 32 : 0);
   auto load_wf = [&](const unsigned short* wtap, int ch) {
-    const char* wb = reinterpret_cast<const char*>(wtap);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)wtap, 0, WTAP, 0x00020000);
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
-      const char* w = wb + (ch * C + (2 * wc + cb) * 16 + l15) * 96 + hf * 48;
-      wf[ch][cb][0] = *reinterpret_cast<const s16x8*>(w + t * 16);
-      wf[ch][cb][1] = *reinterpret_cast<const s16x8*>(w + (t ? 32 : 0));
+      const int so = (ch * C + cb * 16) * 96;
+      wf[ch][cb][0] = __builtin_bit_cast(s16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, wo0, so, 0));
+      wf[ch][cb][1] = __builtin_bit_cast(s16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, wo1, so, 0));
     }
   };
   // the tap after tap j of conv `conv` of member m: the stream runs c1, c2 of each member, then
@@ -492,19 +501,23 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_g(const ResPairParams p)
   // ---- one tap, chunk-major: the MFMAs of chunk ch for every row block of the wave, then chunk ch
   // of the next tap into the fragment registers; hook() once every reload of the tap is issued (its
   // loads are then younger than the fragments the next tap waits for) ----
-  const int soX0 = (hf * 3 + t) * 256, soX1 = (hf * 3 + (t ? 0 : 1)) * 256, soX2 = (hf * 3 + (t ? 0 : 2)) * 256;
+  // lane parts of the three activation reads (piece, row within the 16-row block); a tap adds its
+  // wave-uniform row offset once, and row block / chunk offsets are instruction immediates
+  const int pk0 = ((hf * 3 + t) * NS + l15) * 16, pk1 = ((hf * 3 + (t ? 0 : 1)) * NS + l15) * 16;
+  const int pk2 = ((hf * 3 + (t ? 0 : 2)) * NS + l15) * 16;
   auto tap = [&](f32x4 (&acc)[RB][2], int rowoff, int nrb, const unsigned short* wnext, auto hook) {
+    const int tb = (wr * 16 + rowoff) * 16;
+    const char *xb0 = lds + pk0 + tb, *xb1 = lds + pk1 + tb, *xb2 = lds + pk2 + tb;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
         if (i < nrb) {
-          const int sr = (wr + WR * i) * 16 + l15 + rowoff;
-          const char* xr = lds + (sr >> 4) * BLK + (sr & 15) * 16 + ch * 1536;
-          const s16x8 x2 = *reinterpret_cast<const s16x8*>(xr + soX2);
-          const s16x8 x1 = *reinterpret_cast<const s16x8*>(xr + soX1);
-          const s16x8 x0 = *reinterpret_cast<const s16x8*>(xr + soX0);
+          const int io = (WR * 16 * i) * 16 + ch * 6 * PS;
+          const s16x8 x2 = *reinterpret_cast<const s16x8*>(xb2 + io);
+          const s16x8 x1 = *reinterpret_cast<const s16x8*>(xb1 + io);
+          const s16x8 x0 = *reinterpret_cast<const s16x8*>(xb0 + io);
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) {
             acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][1]),
@@ -585,10 +598,10 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_g(const ResPairParams p)
             mv[e] = (short)mm;
             lv[e] = (short)l;
           }
-          char* dst = lds + (ir >> 4) * BLK + (c0 >> 4) * 1536 + ((c0 >> 3) & 1) * 768 + (ir & 15) * 16 + (c0 & 7) * 2;
+          char* dst = lds + ((c0 >> 4) * 6 + ((c0 >> 3) & 1) * 3) * PS + ir * 16 + (c0 & 7) * 2;
           *reinterpret_cast<s16x4*>(dst) = hv;
-          *reinterpret_cast<s16x4*>(dst + 256) = mv;
-          *reinterpret_cast<s16x4*>(dst + 512) = lv;
+          *reinterpret_cast<s16x4*>(dst + PS) = mv;
+          *reinterpret_cast<s16x4*>(dst + 2 * PS) = lv;
         }
       }
       rp_barrier();
@@ -707,8 +720,8 @@ struct RpGeom4 {
   static constexpr int WC = C / 32, WR = 4 / WC;  // waves: WR row groups x WC column halves
   static constexpr int NB1 = M1 / 16, RB = NB1 / WR;
   static constexpr int NB2 = R / 16;
-  static constexpr int BLK = NCH * 1536;
-  static constexpr int IMG = NS / 16 * BLK;
+  static constexpr int PS = NS * 16;
+  static constexpr int IMG = NCH * 6 * PS;
   static constexpr int G8 = C / 8;
   static constexpr int WTAP = C * C * 6;
   static constexpr int FB = 4;                    // S-image items (8 channels) per thread per load batch
@@ -722,7 +735,7 @@ constexpr int kRp4Rows = C == 32 ? 304 : 112;
 template <int C, bool MEAN, int RR = kRp4Rows<C>>
 __global__ void __launch_bounds__(256, 2) conv_res_pair_w4(const ResPairParams p) {
   using G = RpGeom4<C, RR>;
-  constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB, BLK = G::BLK, IMG = G::IMG;
+  constexpr int R = G::R, NCH = G::NCH, WR = G::WR, RB = G::RB, PS = G::PS, IMG = G::IMG;
   constexpr int G8 = G::G8, NS = G::NS, WTAP = G::WTAP, FB = G::FB;
   __shared__ __attribute__((aligned(16))) char lds[G::LDS];
   float* const bias_lds = reinterpret_cast<float*>(lds + IMG);  // [conv][member][C]
@@ -769,10 +782,10 @@ __global__ void __launch_bounds__(256, 2) conv_res_pair_w4(const ResPairParams p
             mv[e] = (short)m;
             lv[e] = (short)l;
           }
-          char* d = lds + (s >> 4) * BLK + (g8 >> 1) * 1536 + (g8 & 1) * 768 + (s & 15) * 16;
+          char* d = lds + ((g8 >> 1) * 6 + (g8 & 1) * 3) * PS + s * 16;
           *reinterpret_cast<s16x8*>(d) = hv;
-          *reinterpret_cast<s16x8*>(d + 256) = mv;
-          *reinterpret_cast<s16x8*>(d + 512) = lv;
+          *reinterpret_cast<s16x8*>(d + PS) = mv;
+          *reinterpret_cast<s16x8*>(d + 2 * PS) = lv;
         }
       }
     }
@@ -780,13 +793,16 @@ __global__ void __launch_bounds__(256, 2) conv_res_pair_w4(const ResPairParams p
 
   // ---- weight fragments, one tap ahead (conv_res_pair_g) ----
   s16x8 wf[NCH][2][2];
+  // buffer loads: the lane offsets are loop-invariant VGPRs, the tap base a scalar resource and the
+  // chunk / column-block offsets scalar constants, so a reload costs no address arithmetic
+  const int wo0 = ((2 * wc) * 16 + l15) * 96 + hf * 48 + t * 16, wo1 = ((2 * wc) * 16 + l15) * 96 + hf * 48 + (t ? 32 : 0);
   auto load_wf = [&](const unsigned short* wtap, int ch) {
-    const char* wb = reinterpret_cast<const char*>(wtap);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)wtap, 0, WTAP, 0x00020000);
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
-      const char* w = wb + (ch * C + (2 * wc + cb) * 16 + l15) * 96 + hf * 48;
-      wf[ch][cb][0] = *reinterpret_cast<const s16x8*>(w + t * 16);
-      wf[ch][cb][1] = *reinterpret_cast<const s16x8*>(w + (t ? 32 : 0));
+      const int so = (ch * C + cb * 16) * 96;
+      wf[ch][cb][0] = __builtin_bit_cast(s16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, wo0, so, 0));
+      wf[ch][cb][1] = __builtin_bit_cast(s16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, wo1, so, 0));
     }
   };
   auto next_tap = [&](int m, int conv, int j) -> const unsigned short* {
@@ -794,19 +810,23 @@ __global__ void __launch_bounds__(256, 2) conv_res_pair_w4(const ResPairParams p
     if (conv == 0) return p.w2[m];
     return p.w1[m + 1 < nmem ? m + 1 : 0];
   };
-  const int soX0 = (hf * 3 + t) * 256, soX1 = (hf * 3 + (t ? 0 : 1)) * 256, soX2 = (hf * 3 + (t ? 0 : 2)) * 256;
+  // lane parts of the three activation reads (piece, row within the 16-row block); a tap adds its
+  // wave-uniform row offset once, and row block / chunk offsets are instruction immediates
+  const int pk0 = ((hf * 3 + t) * NS + l15) * 16, pk1 = ((hf * 3 + (t ? 0 : 1)) * NS + l15) * 16;
+  const int pk2 = ((hf * 3 + (t ? 0 : 2)) * NS + l15) * 16;
   auto tap = [&](f32x4 (&acc)[RB][2], int rowoff, int nrb, const unsigned short* wnext) {
+    const int tb = (wr * 16 + rowoff) * 16;
+    const char *xb0 = lds + pk0 + tb, *xb1 = lds + pk1 + tb, *xb2 = lds + pk2 + tb;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
         if (i < nrb) {
-          const int sr = (wr + WR * i) * 16 + l15 + rowoff;
-          const char* xr = lds + (sr >> 4) * BLK + (sr & 15) * 16 + ch * 1536;
-          const s16x8 x2 = *reinterpret_cast<const s16x8*>(xr + soX2);
-          const s16x8 x1 = *reinterpret_cast<const s16x8*>(xr + soX1);
-          const s16x8 x0 = *reinterpret_cast<const s16x8*>(xr + soX0);
+          const int io = (WR * 16 * i) * 16 + ch * 6 * PS;
+          const s16x8 x2 = *reinterpret_cast<const s16x8*>(xb2 + io);
+          const s16x8 x1 = *reinterpret_cast<const s16x8*>(xb1 + io);
+          const s16x8 x0 = *reinterpret_cast<const s16x8*>(xb0 + io);
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) {
             acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ch][cb][1]),
@@ -870,10 +890,10 @@ __global__ void __launch_bounds__(256, 2) conv_res_pair_w4(const ResPairParams p
             mv[e] = (short)mm;
             lv[e] = (short)l;
           }
-          char* dst = lds + (ir >> 4) * BLK + (c0 >> 4) * 1536 + ((c0 >> 3) & 1) * 768 + (ir & 15) * 16 + (c0 & 7) * 2;
+          char* dst = lds + ((c0 >> 4) * 6 + ((c0 >> 3) & 1) * 3) * PS + ir * 16 + (c0 & 7) * 2;
           *reinterpret_cast<s16x4*>(dst) = hv;
-          *reinterpret_cast<s16x4*>(dst + 256) = mv;
-          *reinterpret_cast<s16x4*>(dst + 512) = lv;
+          *reinterpret_cast<s16x4*>(dst + PS) = mv;
+          *reinterpret_cast<s16x4*>(dst + 2 * PS) = lv;
         }
       }
       rp_barrier();
