@@ -4,7 +4,9 @@ where the prefilter addresses its input through per-tile buffer descriptors (DES
 exactness is checked there: the codes equal the fp64 argmin of the returned bf16-valued x_pjt_in
 (the reference's search, vector_quantize_pytorch.py:41-45,496-506: first index of the minimum) on a
 row sample that covers the first and last row panels, the last clip entirely, and a stride through
-the rest.  Parity with the reference's CUDA bf16 autocast itself is unpinned (no CPU bf16 path)."""
+the rest.  Parity with the reference's bf16 autocast run is pinned separately on the fixture of the
+reference's own modules under CUDA autocast's op lists (tests/test_gpu_bf16_autocast.py: every module,
+the end-to-end features / codes / decode, and this search on the reference's own x_pjt_in)."""
 import numpy as np
 import pytest
 import torch
