@@ -40,6 +40,8 @@ struct ConvW {
   float* w = nullptr;
   unsigned short* w6 = nullptr;  // bf16 3-plane split, x6 kernel layout
   unsigned short* wc = nullptr;  // 1x1 convs: hi plane only, [Cin/32][Cout][32] (bf16 mode, conv_gemm_bf16dm)
+  unsigned short* w3 = nullptr;  // h3 arithmetic: fp16 h / l of w * 2^w3_shift (ConvParams::w3)
+  int w3_shift = 0;
   float* b = nullptr;
   float* b16 = nullptr;  // the bias rounded to bf16 (bf16 mode: autocast casts it with the weight)
   int cin = 0, cout = 0, taps = 1, phases = 1, in_step = 1, out_mul = 1;
@@ -363,6 +365,32 @@ struct Builder {
           }
     return upload16(out);
   }
+  // fp32 packed [cout][taps][cin] (one phase) -> h3 layout [tap][cin/32][cout][4 groups][h 8 | l 8]
+  // fp16 of w * 2^shift, shift putting the largest |w| in [2^14, 2^15) (conv_gemm_x3dq)
+  unsigned short* h2_pack(const std::vector<float>& pk, int cout, int taps, int cin, int& shift) {
+    if (bad() || dry) return nullptr;
+    float mx = 0.f;
+    for (float v : pk) mx = std::max(mx, std::fabs(v));
+    int e = 0;
+    if (mx > 0.f) std::frexp(mx, &e);  // mx = f * 2^e, f in [0.5, 1)
+    shift = mx > 0.f ? 15 - e : 0;
+    const int nch = cin / 32;
+    std::vector<unsigned short> out((size_t)taps * nch * cout * 64);
+    for (int m = 0; m < taps; ++m)
+      for (int c = 0; c < nch; ++c)
+        for (int o = 0; o < cout; ++o) {
+          unsigned short* dst = &out[(((size_t)m * nch + c) * cout + o) * 64];
+          const float* src = &pk[((size_t)o * taps + m) * cin + c * 32];
+          for (int j = 0; j < 32; ++j) {
+            const float x = std::ldexp(src[j], shift);
+            const _Float16 hh = (_Float16)x;
+            const _Float16 ll = (_Float16)(x - (float)hh);
+            dst[(j >> 3) * 16 + (j & 7)] = __builtin_bit_cast(unsigned short, hh);
+            dst[(j >> 3) * 16 + 8 + (j & 7)] = __builtin_bit_cast(unsigned short, ll);
+          }
+        }
+    return upload16(out);
+  }
   // fp32 packed [cout][cin] (one tap, one phase) -> [cin/32][cout][32] bf16 hi (conv_gemm_bf16dm)
   unsigned short* compact_pack(const std::vector<float>& pk, int cout, int cin) {
     if (bad() || dry) return nullptr;
@@ -421,7 +449,9 @@ struct Builder {
   }
 
   // Conv1d / Linear weight [Cout][Cin][k] -> packed [Cout][k][Cin].
-  ConvW conv(const std::string& prefix, int cin, int cout, int k, int dil, int pad, bool has_bias = true) {
+  // h3: also the h3 weights (conv_gemm_x3dq; the generator's ResBlock convs of the wide stages)
+  ConvW conv(const std::string& prefix, int cin, int cout, int k, int dil, int pad, bool has_bias = true,
+             bool h3 = false) {
     ConvW c;
     c.cin = cin; c.cout = cout; c.taps = k; c.in_step = dil; c.in_base[0] = -pad;
     HostTensor w = weight(prefix, {cout, cin, k});
@@ -433,6 +463,7 @@ struct Builder {
     c.w = upload(pk);
     if (cin % 16 == 0) c.w6 = split_pack(pk, 1, cout, k, cin);
     if (k == 1 && cin % 32 == 0) c.wc = compact_pack(pk, cout, cin);
+    if (h3 && cin % 32 == 0) c.w3 = h2_pack(pk, cout, k, cin, c.w3_shift);
     if (has_bias) {
       c.b = vec(prefix + ".bias", cout);
       c.b16 = vec_bf16(prefix + ".bias", cout);
@@ -541,18 +572,22 @@ int max_gen_width(const dcx_config& c) {  // max over generator layers of channe
 // An activation tensor [rows][C]: fp32 and/or x6 planes ([rows][C/8][3][8] bf16, dcx_planes.h).
 // c1: p holds the compact bf16 layout ([rows][C] hi only; bf16 mode, consumers conv_gemm_bf16dm /
 // vq_prefilter_bk) instead of planes.
+// h2: p holds the fp16 "h2" layout ([rows][C/32][8][8] h and l; the h3 generator arithmetic,
+// consumer conv_gemm_x3dq).
 struct Act {
   float* f = nullptr;
   unsigned short* p = nullptr;
   bool c1 = false;
+  bool h2 = false;
 };
 struct CAct {
   const float* f = nullptr;
   const unsigned short* p = nullptr;
   bool c1 = false;
+  bool h2 = false;
   CAct() = default;
   CAct(const float* f_, const unsigned short* p_, bool c1_ = false) : f(f_), p(p_), c1(c1_) {}
-  CAct(const Act& a) : f(a.f), p(a.p), c1(a.c1) {}
+  CAct(const Act& a) : f(a.f), p(a.p), c1(a.c1), h2(a.h2) {}
 };
 
 // planes layout for every GEMM operand (x6 and bf16 modes)
@@ -574,6 +609,7 @@ struct ConvCall {
   float* y2 = nullptr;           // silu(v), fp32
   unsigned short* y6 = nullptr;  // planes of v
   unsigned short* y6s = nullptr; // planes of silu(v)
+  bool y6s_h2 = false;           // y6s in the h2 layout
   int y6c = 0;                   // y6 layout (ConvParams::y_compact): 0 planes, 1 compact bf16, 2 hm
   float* macc = nullptr;
   const float* res = nullptr;
@@ -581,7 +617,11 @@ struct ConvCall {
   int epi = dcx::EPI_BIAS, mean = dcx::MEAN_NONE;
   bool exact = false;  // keep x6 arithmetic in bf16 mode (the reference's fp32 mel front end)
   bool silu_in = false;  // fp32 input: the conv consumes silu(x) (applied while staging)
-  void silu_to(const Act& a) { y2 = a.f; y6s = a.p; }
+  void silu_to(const Act& a) {
+    y2 = a.f;
+    y6s = a.p;
+    y6s_h2 = a.h2;
+  }
   void out_to(const Act& a) { y = a.f; y6 = a.p; y6c = a.c1 ? 1 : 0; }
 };
 
@@ -602,13 +642,15 @@ int* knob_slot(dcx::Knobs& k, const std::string& n) {
   if (n == "DCX_DWCONV_TILED") return &k.dwconv_tiled;
   if (n == "DCX_SPLIT_MIN_STEPS") return &k.split_min_steps;
   if (n == "DCX_SPLIT_GROUP_OFF") return &k.split_group_off;
+  if (n == "DCX_H3") return &k.h3;
   return nullptr;
 }
 
 void knobs_from_env(dcx::Knobs& k) {
   static const char* const names[] = {"DCX_RP_R",         "DCX_RP_OLD",       "DCX_RP_G64",       "DCX_RP_SYNC",
                                       "DCX_RP_W4",        "DCX_GELU_LUT",     "DCX_BF16_PERSIST", "DCX_BF16_REG_EPI",
-                                      "DCX_DWCONV_TILED", "DCX_SPLIT_MIN_STEPS", "DCX_SPLIT_GROUP_OFF"};
+                                      "DCX_DWCONV_TILED", "DCX_SPLIT_MIN_STEPS", "DCX_SPLIT_GROUP_OFF",
+                                      "DCX_H3"};
   for (const char* n : names) {
     const char* e = std::getenv(n);
     if (e && *e) *knob_slot(k, n) = std::atoi(e);
@@ -655,6 +697,13 @@ int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32,
   p.silu_in = c.silu_in;
   p.x_compact = x6 && c.x.p && c.x.c1 ? 1 : 0;
   p.y_compact = c.y6 ? c.y6c : 0;
+  p.y6s_h2 = c.y6s && c.y6s_h2 ? 1 : 0;
+  if (x6 && c.x.p && c.x.h2) {  // h3 arithmetic (conv_gemm_x3dq)
+    if (!w.w3 || one) return fail(h, DCX_ERR_STATE, "internal: h2 input without h3 weights");
+    p.x_compact = 3;
+    p.w3 = w.w3;
+    p.w3_shift = w.w3_shift;
+  }
   p.wc = one && h->compact ? w.wc : nullptr;
   p.kn = &h->knobs;
   // compact inputs only feed one-product GEMMs; a compact output (the RNE hi value) may also be written
@@ -1216,6 +1265,17 @@ bool res_pair_ok(const dcx_codec* h, int stage) {
   return true;
 }
 
+// Whether generator stage i runs its ResBlock convs in h3 arithmetic (Knobs::h3, x6 mode, not in
+// the split-K latency mode, every conv with h3 weights): their inputs are then written in the h2
+// layout by their producers (ConvT, c1, c2 epilogues).
+bool h3_stage(const dcx_codec* h, int i) {
+  if (!h->knobs.h3 || h->gemm_mode != DCX_GEMM_X6 || h->split_k >= 2) return false;
+  for (int rb = 0; rb < h->cfg.n_res; ++rb)
+    for (int j = 0; j < 3; ++j)
+      if (!h->res[i][rb][j][0].w3 || !h->res[i][rb][j][1].w3) return false;
+  return true;
+}
+
 // Buffers of one generator stage's ParallelBlock (run_parallel_block).
 struct PBlockBufs {
   float* X = nullptr;                // ConvT output: the ResBlocks' input (fp32)
@@ -1378,7 +1438,8 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
     const ConvW& up = h->ups[i];
     const int Co = up.cout, Lo = L * c.up_rates[i];
     const ConvW& rconv = h->res[i][0][0][0];  // every ResBlock conv of the stage has Cin = Cout = Co
-    const Act S_i = in_form(S, up), XS_i = in_form(XS, rconv);
+    const Act S_i = in_form(S, up);
+    Act XS_i = in_form(XS, rconv);
     Act RS_i[NR], Tb_i[NR];
     for (int rb = 0; rb < c.n_res; ++rb) {
       RS_i[rb] = in_form(RS[rb], rconv);
@@ -1387,6 +1448,10 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
     // fp32-input stages: the first conv of each pair applies silu to X / R while staging, so
     // silu(X) and silu(R) are never written (7 activation tensors per stage less HBM traffic)
     const bool silu_on_load = x6_mode(h) && f32_input_ok(rconv);
+    if (h3_stage(h, i)) {  // the ResBlock convs' inputs in the h2 layout (conv_gemm_x3dq)
+      XS_i.h2 = true;
+      for (int rb = 0; rb < c.n_res; ++rb) RS_i[rb].h2 = Tb_i[rb].h2 = true;
+    }
     {
       ConvCall cc = framed(S_i, B, L, C);
       cc.y = X;
@@ -1640,9 +1705,11 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
     const bool silu_on_load = x6_mode(h) && f32_input_ok(w0);
-    const Act XSi = in_form(XS, w0), Tbi = in_form(Tb, w0);
+    Act XSi = in_form(XS, w0), Tbi = in_form(Tb, w0);
+    XSi.h2 = Tbi.h2 = h3_stage(h, a);
     HIPCHK(h, hipMemcpyAsync(y, x, sizeof(float) * M * C, hipMemcpyDeviceToDevice, s));
-    if (!silu_on_load) LAUNCH(h, s, "silu_act", 0, 10.0 * M * C, dcx::launch_silu_act(y, XSi.f, XSi.p, M, C, s));
+    if (!silu_on_load)
+      LAUNCH(h, s, "silu_act", 0, 10.0 * M * C, dcx::launch_silu_act(y, XSi.f, XSi.p, M, C, s, XSi.h2 ? 1 : 0));
     for (int ci = 0; ci < 3; ++ci) {
       ConvCall c1 = framed(silu_on_load ? Act{y, nullptr} : XSi, B, L, C);
       c1.silu_in = silu_on_load;
@@ -1677,12 +1744,16 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
     const bool silu_on_load = x6_mode(h) && f32_input_ok(w0);
     HIPCHK(h, hipMemcpyAsync(X, x, sizeof(float) * per, hipMemcpyDeviceToDevice, s));
     pb.X = X;
+    const bool h3 = h3_stage(h, a);
     pb.XS = in_form(XS, w0);
+    pb.XS.h2 = h3;
     for (int rb = 0; rb < c.n_res; ++rb) {
       pb.RS[rb] = in_form(RS[rb], w0);
       pb.Tb_in[rb] = in_form(pb.Tb[rb], w0);
+      pb.RS[rb].h2 = pb.Tb_in[rb].h2 = h3;
     }
-    if (!silu_on_load) LAUNCH(h, s, "silu_act", 0, 10.0 * per, dcx::launch_silu_act(X, pb.XS.f, pb.XS.p, M, C, s));
+    if (!silu_on_load)
+      LAUNCH(h, s, "silu_act", 0, 10.0 * per, dcx::launch_silu_act(X, pb.XS.f, pb.XS.p, M, C, s, h3 ? 1 : 0));
     pb.Mx = y;
     pb.last = true;
     return run_parallel_block(h, a, B, L, pb, s);
@@ -1957,8 +2028,9 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
         for (int j = 0; j < 3; ++j) {
           const int d = c.res_dilations[rb][j];
           const std::string p = g + "resblocks." + std::to_string(i) + ".blocks." + std::to_string(rb);
-          h->res[i][rb][j][0] = B.conv(p + ".convs1." + std::to_string(j), ch, ch, k, d, (k * d - d) / 2);
-          h->res[i][rb][j][1] = B.conv(p + ".convs2." + std::to_string(j), ch, ch, k, 1, (k - 1) / 2);
+          const bool h3 = ch % 128 == 0;  // the wide stages' convs (conv_gemm_x3dq tiles)
+          h->res[i][rb][j][0] = B.conv(p + ".convs1." + std::to_string(j), ch, ch, k, d, (k * d - d) / 2, true, h3);
+          h->res[i][rb][j][1] = B.conv(p + ".convs2." + std::to_string(j), ch, ch, k, 1, (k - 1) / 2, true, h3);
         }
       }
     }

@@ -281,7 +281,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
   const int lrow = lane & 31, rhalf = 4 * (lane >> 5);
   const long long ob = (long long)b * p.y_bstride;
   unsigned short* y6 = p.y6 ? p.y6 + ob * (p.y_compact == 1 ? 1 : p.y_compact == 2 ? 2 : 3) : nullptr;
-  unsigned short* y6s = p.y6s ? p.y6s + ob * 3 : nullptr;
+  unsigned short* y6s = p.y6s ? p.y6s + ob * (p.y6s_h2 ? 2 : 3) : nullptr;
   // Each thread finishes G consecutive output channels of a row (G = 8: 16-byte plane / compact
   // stores; the epilogue's store issue, not its bytes, sets its pace), the same channels for every
   // row, so bias and gamma are loaded once per tile.
@@ -459,7 +459,10 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
             *reinterpret_cast<f32x4*>(p.y2 + o) = f32x4{sv[0], sv[1], sv[2], sv[3]};
             *reinterpret_cast<f32x4*>(p.y2 + o + 4) = f32x4{sv[4], sv[5], sv[6], sv[7]};
           }
-          if (y6s) store_planes8(y6s, orow, p.Cout, co, sv);
+          if (y6s) {
+            if (p.y6s_h2) store_h2_8(y6s, orow, p.Cout, co, sv);
+            else store_planes8(y6s, orow, p.Cout, co, sv);
+          }
         }
       } else {
         if (y6) {
@@ -472,7 +475,10 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
 #pragma unroll
           for (int e = 0; e < 4; ++e) sv[e] = p.round_bf16 ? bf16_val(bf16_bits(silu_f(x[0][e]))) : silu_f(x[0][e]);
           if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
-          if (y6s) store_planes4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+          if (y6s) {
+            if (p.y6s_h2) store_h2_4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+            else store_planes4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+          }
         }
       }
     }
@@ -551,7 +557,8 @@ __device__ __forceinline__ void splitk_epi4(const ConvParams& p, const float* __
 #pragma unroll
     for (int e = 0; e < 4; ++e) sv[e] = silu_f(x[e]);
     if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
-    if (p.y6s) store_planes4(p.y6s + ob * 3, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+    if (p.y6s && p.y6s_h2) store_h2_4(p.y6s + ob * 2, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+    else if (p.y6s) store_planes4(p.y6s + ob * 3, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
   }
 }
 
@@ -2308,6 +2315,228 @@ static hipError_t launch_x6dq(const ConvParams& p, int batch, int phases, hipStr
 }
 
 // ---------------------------------------------------------------------------------------------
+// conv_gemm_x3dq: the fp16 "h3" arithmetic (round 5) on conv_gemm_x6dq's LDS-DMA ping-pong schedule.
+//
+// An fp32 value is held as two fp16 values, h = fp16(x) and l = fp16(x - h) (dcx_planes.h "h2"
+// layout, 22 significant bits), the weights likewise after scaling by 2^w3_shift (the largest |w|
+// just below 2^15, so l stays normal for all weights within 2^-18 of it); the accumulators are
+// scaled back by 2^-w3_shift before the epilogue.  A product keeps three terms, hh' + hl' + lh'
+// (ll' is 2^-22 relative), against x6's six, at the same K32 rate per MFMA
+// (v_mfma_f32_16x16x32_f16; the K16 f16 MFMA issues at half rate on gfx950, tools/probe).
+// A step is one 32-channel chunk of one tap; per 16 x 16 block three MFMAs, with the lane's
+// K group kg = lane >> 4 = (t, hf) = (lane >> 5, (lane >> 4) & 1):
+//   S1: A{h, group kg} . B{h', group kg}                                  = hh'
+//   S2: A{t ? l : h, group hf} . B{t ? h' : l', group hf}                 = hl' + lh' (groups 0, 1)
+//   S3: the same for groups 2 + hf                                        = hl' + lh' (groups 2, 3)
+// Tiles BM x BN = 128 x 256 (BN = 256) or 256 x 128, 8 waves of 64 x 64 (group 0 the upper half of
+// the rows); every fragment of a step (12 A + 12 B ds_read_b128) is read in the memory segment and
+// an MFMA segment is 48 MFMAs.  LDS images, piece-major and row-linear: A [piece 8][BM + 64][16 B]
+// (two buffers, by chunk parity), B [piece 8][BN][16 B] (3-slot ring), piece = plane * 4 + channel
+// group; one 1 KiB DMA instruction fills 64 rows of one piece.  Rows of one piece are 16 B apart,
+// so a ds_read_b128 lane group (16 distinct rows mod 16) is conflict-free at any tap offset.
+// The A buffer of chunk c + 2 is issued taps - 2 segments after chunk c's last read: taps >= 3.
+// ---------------------------------------------------------------------------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+template <int BN>
+__device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, const int b, const int ph) {
+  constexpr int HALO = 64;
+  constexpr int BM = 32768 / BN, WN = BN / 64, WM = 8 / WN;
+  constexpr int WR = BM / WM, WC = BN / WN, TM = WR / 16, TN = WC / 16;
+  constexpr int AR = BM + HALO;                 // rows of an input image
+  constexpr int A_G = AR / 16, B_G = BN / 16;   // 1 KiB DMA instructions per group (A per chunk, B per step)
+  constexpr int A_PW = A_G / 4, B_PW = B_G / 4;
+  constexpr int ABUF = AR * 128, BBUF = BN * 128;  // bytes
+  constexpr int LDS_B = 2 * ABUF + 3 * BBUF;
+  static_assert(WR == 64 && WC == 64 && A_G % 4 == 0 && B_G % 4 == 0 && AR % 64 == 0, "tile shape");
+  static_assert(LDS_B <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned short lds[LDS_B / 2];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int group = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int wm = wave / WN, wn = wave % WN;
+  const int ntiles = p.Cout / BN;
+  const int mt = wg / ntiles, nt = wg - mt * ntiles;
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int nchunks = p.Cin / 32;
+  const int taps = p.taps;
+  const int nsteps = nchunks * taps;
+  const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
+  const int row0 = q0 + p.in_base[ph] + lo_rel;
+  const int arow = p.ldx * 4;  // bytes per h2 row
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.x6 + (long long)b * p.x_bstride * 2), 0, p.Lin * arow, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.w3 + (long long)ph * taps * nchunks * p.Cout * 64), 0, taps * nchunks * p.Cout * 128, 0x00020000);
+
+  // DMA: group instruction k fills 64 rows of piece (k * 64) / rows; the wave's i-th is k = i * 4 + gw.
+  // Source of piece pc in an h2 row's chunk: channel group pc & 3 at 32 B, plane pc >> 2 at 16 B.
+  int a_off[A_PW], b_off[B_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int u = (group * A_G + i * 4 + gw) * 64;
+    const int pc = u / AR, row = u - pc * AR + lane;
+    a_off[i] = (row0 + row) * arow + (pc & 3) * 32 + (pc >> 2) * 16;  // negative rows: out of range
+  }
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int u = (group * B_G + i * 4 + gw) * 64;
+    const int pc = u / BN, col = u - pc * BN + lane;
+    b_off[i] = (co0 + col) * 128 + (pc & 3) * 32 + (pc >> 2) * 16;
+  }
+  unsigned short* const a_dst = lds + (group * A_G + gw) * 512;
+  unsigned short* const b_dst = lds + ABUF + (group * B_G + gw) * 512;  // ushorts: 2 * ABUF bytes
+  auto dma_step = [&](int c, int m, int slot) {
+    int n = B_PW;
+    if (m == 0) {
+#pragma unroll
+      for (int i = 0; i < A_PW; ++i) dma16(rx, a_dst + (c & 1) * (ABUF / 2) + i * 2048, a_off[i] + c * 128, 0);
+      n += A_PW;
+    }
+    const int soff = (m * nchunks + c) * p.Cout * 128;
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) dma16(rw, b_dst + slot * (BBUF / 2) + i * 2048, b_off[i], soff);
+    return n;
+  };
+
+  const int l15 = lane & 15, hf = (lane >> 4) & 1, t = lane >> 5, kg = lane >> 4;
+  // piece offsets (bytes) of the lane's three operand sets
+  const int pa0 = kg * AR * 16, pa1 = (t * 4 + hf) * AR * 16, pa2 = (t * 4 + 2 + hf) * AR * 16;
+  const int pb0 = kg * BN * 16, pb1 = ((1 - t) * 4 + hf) * BN * 16, pb2 = ((1 - t) * 4 + 2 + hf) * BN * 16;
+  const char* const ldsb = reinterpret_cast<const char*>(lds);
+  const int bcol = 2 * ABUF + (wn * WC + l15) * 16;
+  s16x8 aq[TM][3], bq[TN][3];
+  auto readF = [&](int c, int m, int slot) {
+    const char* a = ldsb + (c & 1) * ABUF + (wm * WR + m * p.in_step - lo_rel + l15) * 16;
+    const char* bb = ldsb + bcol + slot * BBUF;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bq[j][0] = *reinterpret_cast<const s16x8*>(bb + j * 256 + pb0);
+      bq[j][1] = *reinterpret_cast<const s16x8*>(bb + j * 256 + pb1);
+      bq[j][2] = *reinterpret_cast<const s16x8*>(bb + j * 256 + pb2);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      aq[i][0] = *reinterpret_cast<const s16x8*>(a + i * 256 + pa0);
+      aq[i][1] = *reinterpret_cast<const s16x8*>(a + i * 256 + pa1);
+      aq[i][2] = *reinterpret_cast<const s16x8*>(a + i * 256 + pa2);
+    }
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the cross terms first (S2, S3), then hh'; 16 independent accumulators between dependent MFMAs
+  auto mfma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int set = k == 2 ? 0 : k + 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, aq[i][set]),
+                                                             __builtin_bit_cast(f16x8, bq[j][set]), acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto adv = [&](int& c_, int& m_) {
+    if (++m_ == taps) { m_ = 0; ++c_; }
+  };
+  auto inc3 = [](int& slot) { slot = slot == 2 ? 0 : slot + 1; };
+
+  int cl = 0, ml = 0;
+  for (int tt = 0; tt < 3; ++tt) {
+    if (tt < nsteps) dma_step(cl, ml, tt);
+    adv(cl, ml);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  seg_barrier();
+  int cr = 0, mr = 0;
+  if (group == 0) {
+    readF(0, 0, 0);
+    adv(cr, mr);
+    int rs = 1, ws = 0;  // slot of the step read next (s + 1), of the step issued next (s + 3)
+    for (int s = 0; s < nsteps; ++s) {
+      mfma();  // MFMA(s)
+      seg_barrier();
+      // MEM0(s): fragments of step s + 1, issue step s + 3, retire step s + 2
+      if (s + 1 < nsteps) readF(cr, mr, rs);
+      int n = 0;
+      if (s + 3 < nsteps) n = dma_step(cl, ml, ws);
+      wait_dma(n);
+      seg_barrier();
+      adv(cr, mr);
+      adv(cl, ml);
+      inc3(rs);
+      inc3(ws);
+    }
+  } else {
+    int rs = 0, ws = 0;  // slot of step s, of step s + 2
+    for (int s = 0; s < nsteps; ++s) {
+      // MEM1(s): fragments of step s, issue step s + 2 (s >= 1), retire step s + 1
+      readF(cr, mr, rs);
+      int n = 0;
+      if (s >= 1 && s + 2 < nsteps) {
+        n = dma_step(cl, ml, ws);
+        adv(cl, ml);
+      }
+      wait_dma(n);
+      seg_barrier();
+      mfma();  // MFMA(s)
+      seg_barrier();
+      adv(cr, mr);
+      inc3(rs);
+      if (s >= 1) inc3(ws);
+      else ws = 0;  // step 3's slot
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // undo the weight scaling (a power of two: exact)
+  const float unscale = __builtin_ldexpf(1.0f, -p.w3_shift);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] *= unscale;
+  epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+}
+
+template <int BN>
+__global__ void __launch_bounds__(512, 2) conv_gemm_x3dq(const ConvParams p) {
+  int wg, b, ph;
+  flat_tile(((p.Lq + 32768 / BN - 1) / (32768 / BN)) * (p.Cout / BN), p.batch, wg, b, ph);
+  x3dq_tile<BN>(p, wg, b, ph);
+}
+
+// grouped launch of up to 3 h3 convs (conv_gemm_x6dq_group's member mapping)
+template <int BN>
+__global__ void __launch_bounds__(512, 2) conv_gemm_x3dq_group(const ConvGroup g) {
+  const int t = blockIdx.x;
+  const int k = t >= g.start[1] ? (t >= g.start[2] ? 2 : 1) : 0;
+  const int local = xcd_remap(t - g.start[k], g.start[k + 1] - g.start[k]);
+  const int b = local / g.tiles_per_clip[k];
+  ConvParams p;
+  if (k == 0) p = g.p[0];
+  else if (k == 1) p = g.p[1];
+  else p = g.p[2];
+  x3dq_tile<BN>(p, local - b * g.tiles_per_clip[k], b, 0);
+}
+
+// Whether conv_gemm_x3dq<bn> takes an h3 conv (input in the h2 layout, x_compact == 3).
+static bool x3dq_ok(const ConvParams& p, int bn) {
+  const int span = (p.taps - 1) * (p.in_step < 0 ? -p.in_step : p.in_step);
+  if (!p.x6 || !p.w3 || p.x_compact != 3 || p.Cin % 32 || p.Cout % bn || p.taps < 3 || span == 0 || span > 64 ||
+      p.ksplit > 1)
+    return false;
+  const long long arow = (long long)p.ldx * 4;
+  return (long long)(p.Lin + 1024) * arow < (1LL << 31) && (long long)p.taps * p.Cin * p.Cout * 4 < (1LL << 31);
+}
+static int x3dq_bn(const ConvParams& p) { return p.Cout % 256 == 0 ? 256 : 128; }
+
+// ---------------------------------------------------------------------------------------------
 // conv_gemm_bf16dm: the DCX_GEMM_BF16 mode's 1x1 convs (one hi * hi' product, the reference's
 // enable_bfloat16 autocast) on the LDS-DMA ping-pong schedule of conv_gemm_x6dm.
 //
@@ -3828,8 +4057,25 @@ bool bf16dm_takes(int cin, int cout, int lq, int ldx, int phases) {
          (long long)(cin / 16) * cout * 96 < (1LL << 31);
 }
 
+template <int BN>
+static hipError_t launch_x3dq(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
+  constexpr int BM = 32768 / BN;
+  const dim3 grid((unsigned)(((p.Lq + BM - 1) / BM) * (p.Cout / BN) * batch * phases));
+  ConvParams q = p;
+  q.batch = batch;
+  q.phases = phases;
+  if (kname) *kname = BN == 256 ? "conv_gemm_x3dq<128,256,halo>" : "conv_gemm_x3dq<256,128,halo>";
+  hipLaunchKernelGGL((conv_gemm_x3dq<BN>), grid, dim3(512), 0, s, q);
+  return hipGetLastError();
+}
+
 hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s, const char** kname) {
   if (p.Cin % BK || p.Cout % 32 || phases < 1 || phases > kMaxPhases) return hipErrorInvalidValue;
+  if (p.x_compact == 3) {  // h2 input: the h3 kernels only
+    const int bn = x3dq_bn(p);
+    if (!x3dq_ok(p, bn)) return hipErrorInvalidValue;
+    return bn == 256 ? launch_x3dq<256>(p, batch, phases, s, kname) : launch_x3dq<128>(p, batch, phases, s, kname);
+  }
   if (p.w6) {
     if (p.nprod != 6 && p.nprod != 1) return hipErrorInvalidValue;
     // split-K runs on conv_gemm_x6pp / x6lm (the kernels that read ksplit), whatever the tile count
@@ -3955,11 +4201,39 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
 hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t s, const char** kname) {
   if (n < 1 || n > kMaxGroup || batch < 1) return hipErrorInvalidValue;
   const int cout = ps[0].Cout;
+  if (ps[0].x_compact == 3) {  // h3 convs: conv_gemm_x3dq_group (any tile count)
+    const int bn = x3dq_bn(ps[0]), bm = 32768 / bn;
+    for (int i = 0; i < n; ++i)
+      if (ps[i].Cout != cout || ps[i].x_compact != 3 || !x3dq_ok(ps[i], bn)) return hipErrorNotSupported;
+    int order[kMaxGroup] = {0, 1, 2};
+    for (int i = 0; i < n; ++i)
+      for (int j = i + 1; j < n; ++j)
+        if (ps[order[j]].taps > ps[order[i]].taps) std::swap(order[i], order[j]);
+    ConvGroup g{};
+    long long start = 0;
+    for (int k = 0; k < n; ++k) {
+      const ConvParams& p = ps[order[k]];
+      g.p[k] = p;
+      g.tiles_per_clip[k] = ((p.Lq + bm - 1) / bm) * (cout / bn);
+      g.start[k] = (int)start;
+      start += (long long)g.tiles_per_clip[k] * batch;
+    }
+    if (start > (1LL << 30)) return hipErrorInvalidValue;
+    for (int k = n; k <= kMaxGroup; ++k) g.start[k] = (int)start;
+    if (bn == 256) {
+      if (kname) *kname = "conv_gemm_x3dq_group<128,256,halo>";
+      hipLaunchKernelGGL((conv_gemm_x3dq_group<256>), dim3((unsigned)start), dim3(512), 0, s, g);
+    } else {
+      if (kname) *kname = "conv_gemm_x3dq_group<256,128,halo>";
+      hipLaunchKernelGGL((conv_gemm_x3dq_group<128>), dim3((unsigned)start), dim3(512), 0, s, g);
+    }
+    return hipGetLastError();
+  }
   const int bn = cout % 256 == 0 ? 256 : 128, bm = 65536 / bn;
   // every member must be one launch_conv would give to conv_gemm_x6dq<bn> (same bits either way)
   for (int i = 0; i < n; ++i) {
     const ConvParams& p = ps[i];
-    if (p.Cout != cout || cout % 128 || p.Cin % BK || !p.x6 || !p.w6 || p.nprod != 6 || p.taps < 3 ||
+    if (p.Cout != cout || cout % 128 || p.Cin % BK || !p.x6 || !p.w6 || p.nprod != 6 || p.x_compact || p.taps < 3 ||
         tap_span(p) == 0 || tap_span(p) > 64 || (p.Cin / BK) * p.taps % 2 || !x6dm_ok(p, true, bn) ||
         !big_tiles_pay(p, 1, bn))
       return hipErrorNotSupported;

@@ -36,6 +36,7 @@ struct Knobs {
   int dwconv_tiled = 0;     // DCX_DWCONV_TILED=1: the round-2 tiled dwconv_ln (same bits)
   int split_min_steps = 0;  // DCX_SPLIT_MIN_STEPS: split-K only convs with at least this many K steps
   int split_group_off = 0;  // DCX_SPLIT_GROUP_OFF=1: per-conv split launches instead of grouped ones
+  int h3 = 0;               // DCX_H3=1: the wide generator stages' ResBlock convs in h3 arithmetic (x6 mode)
 };
 
 // out[b][q*out_mul + phase][co] = epi( sum_{m<taps} sum_{ci<Cin} x[b][q + in_base[phase] + m*in_step][ci]
@@ -81,7 +82,8 @@ struct ConvParams {
   //   1 = compact bf16 ([rows][C], hi plane only; bf16 mode; read by conv_gemm_bf16dm and
   //       vq_prefilter_bk; written with round_bf16, ldy == Cout);
   //   2 = "hm" ([rows][C/32][8][8], hi and mid planes per 32 channels; x6-mode x_pjt_in, read by
-  //       vq_prefilter_dm only).
+  //       vq_prefilter_dm only);
+  //   3 = "h2" (x only: [rows][C/32][8][8] fp16 h and l per 32 channels; read by conv_gemm_x3dq).
   int x_compact, y_compact;
   // bf16-mode 1x1 weights as [phase][Cin/32][Cout][32] bf16 (hi only; conv_gemm_bf16dm), or null;
   // for the VQ prefilter: the codebook as launch_repack_codebook_bk writes it.
@@ -99,6 +101,12 @@ struct ConvParams {
   int gelu_lut;
   // the handle's switches (host only; null = the defaults)
   const Knobs* kn;
+  // h3 arithmetic (conv_gemm_x3dq, x_compact == 3: the input in the fp16 "h2" layout of
+  // dcx_planes.h): weights [phase][tap][Cin/32][Cout][4 groups][h 8 | l 8] fp16 of w * 2^w3_shift
+  const unsigned short* w3;
+  int w3_shift;
+  // y6s in the h2 layout instead of planes (the input of a following h3 conv)
+  int y6s_h2;
 };
 
 // Independent convs issued as one launch (launch_conv_group); problem k owns logical tiles
@@ -245,7 +253,9 @@ bool vq_bk_takes(int ncodes, int dim);
 bool vq_hm_takes(int ncodes, int dim, long long rows);
 hipError_t launch_frame_pad(const float* audio, float* frames, unsigned short* frames6, int batch, long long n, int rows,
                             int hop, int pad_left, hipStream_t s);
-hipError_t launch_silu_act(const float* x, float* yf, unsigned short* y6, long long rows, int C, hipStream_t s);
+// h2: y6 in the h2 layout (dcx_planes.h) instead of planes
+hipError_t launch_silu_act(const float* x, float* yf, unsigned short* y6, long long rows, int C, hipStream_t s,
+                           int h2 = 0);
 hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, float* loglin, long long rows, int nbins,
                            int ld_out, hipStream_t s);
 hipError_t launch_split_planes(const float* x, unsigned short* y6, long long rows, int C, int compact, hipStream_t s);

@@ -373,7 +373,8 @@ hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, 
 // silu(x) as fp32 and/or planes (dcx_module_forward's ResBlock / ParallelBlock entries: the
 // generator itself produces these in conv epilogues).  Same arithmetic as the epilogues' silu.
 __global__ void __launch_bounds__(256) silu_act_kernel(const float* __restrict__ x, float* __restrict__ yf,
-                                                        unsigned short* __restrict__ y6, long long rows, int C) {
+                                                        unsigned short* __restrict__ y6, long long rows, int C,
+                                                        int h2) {
   const long long total4 = rows * C / 4;
   for (long long i4 = (long long)blockIdx.x * 256 + threadIdx.x; i4 < total4; i4 += (long long)gridDim.x * 256) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(x + i4 * 4);
@@ -381,17 +382,18 @@ __global__ void __launch_bounds__(256) silu_act_kernel(const float* __restrict__
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = v[e] * __builtin_amdgcn_rcpf(1.0f + __expf(-v[e]));
     if (yf) *reinterpret_cast<f32x4*>(yf + i4 * 4) = f32x4{o[0], o[1], o[2], o[3]};
-    if (y6) store_planes4(y6, (i4 * 4) / C, C, (int)((i4 * 4) % C), o[0], o[1], o[2], o[3]);
+    if (y6 && h2) store_h2_4(y6, (i4 * 4) / C, C, (int)((i4 * 4) % C), o[0], o[1], o[2], o[3]);
+    else if (y6) store_planes4(y6, (i4 * 4) / C, C, (int)((i4 * 4) % C), o[0], o[1], o[2], o[3]);
   }
 }
 
-hipError_t launch_silu_act(const float* x, float* yf, unsigned short* y6, long long rows, int C, hipStream_t s) {
-  if (C % 8 || rows < 0) return hipErrorInvalidValue;
+hipError_t launch_silu_act(const float* x, float* yf, unsigned short* y6, long long rows, int C, hipStream_t s, int h2) {
+  if (C % 8 || rows < 0 || (h2 && C % 32)) return hipErrorInvalidValue;
   const long long total4 = rows * C / 4;
   if (total4 == 0) return hipSuccess;
   const long long nb = (total4 + 255) / 256;
   const unsigned g = (unsigned)(nb < 8192 ? nb : 8192);
-  hipLaunchKernelGGL(silu_act_kernel, dim3(g), dim3(256), 0, s, x, yf, y6, rows, C);
+  hipLaunchKernelGGL(silu_act_kernel, dim3(g), dim3(256), 0, s, x, yf, y6, rows, C, h2);
   return hipGetLastError();
 }
 

@@ -1,0 +1,95 @@
+"""The h3 arithmetic of the wide generator stages (Knobs::h3, DCX_H3=1; conv_gemm_x3dq).
+
+The ResBlock convs of the C = 512 / 256 / 128 stages take their inputs as two fp16 values
+(h = fp16(x), l = fp16(x - h): 22 significant bits) and the weights likewise after a power-of-two
+scale, and sum hh' + hl' + lh' in fp32 (half the MFMAs of x6).  Bounds:
+  * a stage's ParallelBlock against the fp64 oracle: max relative error < 2e-4, the bound the x6
+    path is held to (tests/test_gpu_modules.py), and within 4x of the x6 path's own error;
+  * the generator output against the x6 path on the same input: SNR >= 100 dB (fp32-level
+    agreement; two fp32-accurate sums in different orders), and against the reference's waveform
+    fixtures >= 80 dB as the x6 path (tests/test_gpu_stages.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.abs(a - b).max() / (np.abs(b).max() + 1e-30)
+
+
+def _snr(x, ref):
+    x = np.asarray(x, np.float64)
+    ref = np.asarray(ref, np.float64)
+    return 10 * np.log10((ref ** 2).sum() / max(((x - ref) ** 2).sum(), 1e-300))
+
+
+@pytest.fixture(scope="module")
+def eng(cfg, state):
+    from distilcodec_nabeel_amd.engine import NativeCodec
+
+    return NativeCodec(cfg, state, "cuda:0", gemm="x6")
+
+
+def _cl(x):
+    return torch.from_numpy(np.ascontiguousarray(x.transpose(0, 2, 1))).to("cuda:0")
+
+
+@pytest.mark.parametrize("stage", [0, 1, 2])
+def test_parallel_block_h3_vs_oracle(eng, state, cfg, stage):
+    from oracle import reference_cpu as R
+
+    C = cfg["decoder"]["upsample_initial_channel"] >> (stage + 1)
+    x = torch.from_numpy(np.random.default_rng(10 + stage).standard_normal((2, C, 300)).astype(np.float32))
+    ref = torch.nn.functional.silu(R.parallel_block(x.double(), state["generator"], stage, cfg["decoder"], torch.float64))
+    ref = ref.numpy()
+    y6 = eng.module(f"generator.resblocks.{stage}", _cl(x.numpy())).cpu().numpy().transpose(0, 2, 1)
+    with eng.knobs(DCX_H3=1):
+        y3 = eng.module(f"generator.resblocks.{stage}", _cl(x.numpy())).cpu().numpy().transpose(0, 2, 1)
+    e6, e3 = _rel(y6, ref), _rel(y3, ref)
+    print(f"\nstage {stage} (C = {C}): x6 rel err {e6:.3g}, h3 rel err {e3:.3g}")
+    assert e3 < 2e-4
+    assert e3 < 4 * max(e6, 1e-7)
+
+
+@pytest.mark.parametrize("stage", [0, 2])
+def test_resblock_h3_vs_oracle(eng, state, cfg, stage):
+    """One ResBlock1 (the per-module path: silu_act writes the h2 input)."""
+    from oracle import reference_cpu as R
+
+    C = cfg["decoder"]["upsample_initial_channel"] >> (stage + 1)
+    x = torch.from_numpy(np.random.default_rng(20 + stage).standard_normal((1, C, 257)).astype(np.float32))
+    d = cfg["decoder"]
+    k, dils = d["resblock_kernel_sizes"][2], d["resblock_dilation_sizes"][2]
+    ref = R._resblock1(x.double(), state["generator"], f"resblocks.{stage}.blocks.2", k, dils, torch.float64).numpy()
+    with eng.knobs(DCX_H3=1):
+        y3 = eng.module(f"generator.resblocks.{stage}.blocks.2", _cl(x.numpy())).cpu().numpy().transpose(0, 2, 1)
+    assert _rel(y3, ref) < 2e-4
+
+
+def test_generator_h3_vs_x6(eng, golden):
+    for name in ("e2e_batch", "e2e_real"):
+        g = golden[name]
+        z = torch.from_numpy(g["quantized"]).transpose(1, 2)
+        w6 = eng.generate(z).cpu().numpy()
+        with eng.knobs(DCX_H3=1):
+            w3 = eng.generate(z).cpu().numpy()
+        s36, s3r = _snr(w3, w6), _snr(w3, g["wav"])
+        print(f"\n{name}: h3 vs x6 {s36:.1f} dB, h3 vs reference {s3r:.1f} dB (x6 vs reference {_snr(w6, g['wav']):.1f})")
+        assert s36 >= 100, (name, s36)
+        assert s3r >= 80, (name, s3r)
+
+
+def test_h3_knob_off_is_x6_bits(eng, golden):
+    """The knob switches kernels only where it says: off again gives the x6 path's bits."""
+    g = golden["e2e_3s"]
+    z = torch.from_numpy(g["quantized"]).transpose(1, 2)
+    a = eng.generate(z).cpu().numpy()
+    with eng.knobs(DCX_H3=1):
+        eng.generate(z)
+    b = eng.generate(z).cpu().numpy()
+    assert np.array_equal(a, b)
