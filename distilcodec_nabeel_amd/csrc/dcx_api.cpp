@@ -515,8 +515,8 @@ struct Builder {
     }
     b.dwb = vec(p + ".dwconv.bias", C);
     b.ln = ln(p + ".norm", C);
-    b.pw1 = conv(p + ".pwconv1", C, 4 * C, 1, 1, 0);
-    b.pw2 = conv(p + ".pwconv2", 4 * C, C, 1, 1, 0);
+    b.pw1 = conv(p + ".pwconv1", C, 4 * C, 1, 1, 0, true, true);
+    b.pw2 = conv(p + ".pwconv2", 4 * C, C, 1, 1, 0, true, true);
     b.gamma = vec(p + ".gamma", C);
     return b;
   }
@@ -610,7 +610,7 @@ struct ConvCall {
   unsigned short* y6 = nullptr;  // planes of v
   unsigned short* y6s = nullptr; // planes of silu(v)
   bool y6s_h2 = false;           // y6s in the h2 layout
-  int y6c = 0;                   // y6 layout (ConvParams::y_compact): 0 planes, 1 compact bf16, 2 hm
+  int y6c = 0;                   // y6 layout (ConvParams::y_compact): 0 planes, 1 compact bf16, 2 hm, 3 h2
   float* macc = nullptr;
   const float* res = nullptr;
   const float* gamma = nullptr;
@@ -622,7 +622,7 @@ struct ConvCall {
     y6s = a.p;
     y6s_h2 = a.h2;
   }
-  void out_to(const Act& a) { y = a.f; y6 = a.p; y6c = a.c1 ? 1 : 0; }
+  void out_to(const Act& a) { y = a.f; y6 = a.p; y6c = a.c1 ? 1 : a.h2 ? 3 : 0; }
 };
 
 // Planes-mode convs with Cout <= 64, Cin <= 128 and a tap halo take an fp32 input (split while
@@ -643,6 +643,8 @@ int* knob_slot(dcx::Knobs& k, const std::string& n) {
   if (n == "DCX_SPLIT_MIN_STEPS") return &k.split_min_steps;
   if (n == "DCX_SPLIT_GROUP_OFF") return &k.split_group_off;
   if (n == "DCX_H3") return &k.h3;
+  if (n == "DCX_H3_BN") return &k.h3_bn;
+  if (n == "DCX_H3_1X1") return &k.h3_1x1;
   return nullptr;
 }
 
@@ -650,7 +652,7 @@ void knobs_from_env(dcx::Knobs& k) {
   static const char* const names[] = {"DCX_RP_R",         "DCX_RP_OLD",       "DCX_RP_G64",       "DCX_RP_SYNC",
                                       "DCX_RP_W4",        "DCX_GELU_LUT",     "DCX_BF16_PERSIST", "DCX_BF16_REG_EPI",
                                       "DCX_DWCONV_TILED", "DCX_SPLIT_MIN_STEPS", "DCX_SPLIT_GROUP_OFF",
-                                      "DCX_H3"};
+                                      "DCX_H3",           "DCX_H3_BN",        "DCX_H3_1X1"};
   for (const char* n : names) {
     const char* e = std::getenv(n);
     if (e && *e) *knob_slot(k, n) = std::atoi(e);
@@ -710,6 +712,7 @@ int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32,
   // in x6 mode (x_pjt_in for vq_prefilter_b1)
   if (p.x_compact == 1 && !one) return fail(h, DCX_ERR_STATE, "internal: compact layout outside bf16 mode");
   if (p.y_compact == 2 && (!x6 || one)) return fail(h, DCX_ERR_STATE, "internal: hm layout outside x6 mode");
+  if (p.y_compact == 3 && (!x6 || one)) return fail(h, DCX_ERR_STATE, "internal: h2 layout outside x6 mode");
   return DCX_OK;
 }
 
@@ -718,6 +721,13 @@ int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32,
 bool takes_compact(const dcx_codec* h, const ConvW& w, long long rows) {
   return h->compact && h->gemm_mode == DCX_GEMM_BF16 && w.wc && w.taps == 1 && w.phases == 1 && w.in_base[0] == 0 &&
          rows < (1LL << 31) && dcx::bf16dm_takes(w.cin, w.cout, (int)rows, w.cin, 1);
+}
+
+// Whether a one-tap conv runs in h3 arithmetic (conv_gemm_x3dm; Knobs::h3_1x1, x6 mode, not in the
+// split-K latency mode), so its producer writes the h2 layout.
+bool takes_h3(const dcx_codec* h, const ConvW& w) {
+  return h->knobs.h3_1x1 && h->gemm_mode == DCX_GEMM_X6 && h->split_k < 2 && w.w3 && w.taps == 1 && w.phases == 1 &&
+         w.in_base[0] == 0 && w.cout % 128 == 0;
 }
 
 // algorithmic FLOPs and bytes of one conv (profiling)
@@ -988,8 +998,10 @@ int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, in
   const int C = bw.C;
   ln.c1 = ln.p && takes_compact(h, bw.pw1, M);
   hid.c1 = hid.p && takes_compact(h, bw.pw2, M);
+  ln.h2 = ln.p && takes_h3(h, bw.pw1);
+  hid.h2 = hid.p && takes_h3(h, bw.pw2);
   LAUNCH(h, s, "dwconv_ln", 14.0 * M * C, 8.0 * M * C,
-         dcx::launch_dwconv_ln(x, ln.f, ln.p, ln.c1 ? 1 : 0, bw.dww, bw.dwb, bw.ln.w, bw.ln.b, B, T, C,
+         dcx::launch_dwconv_ln(x, ln.f, ln.p, ln.c1 ? 1 : ln.h2 ? 3 : 0, bw.dww, bw.dwb, bw.ln.w, bw.ln.b, B, T, C,
                                h->gemm_mode == DCX_GEMM_BF16 ? 1 : 0, &h->knobs, s));
   ConvCall c1 = pointwise(ln, M);
   c1.out_to(hid);

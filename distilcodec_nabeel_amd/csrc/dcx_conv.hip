@@ -280,7 +280,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
   const int wm = wave / WN, wn = wave % WN;
   const int lrow = lane & 31, rhalf = 4 * (lane >> 5);
   const long long ob = (long long)b * p.y_bstride;
-  unsigned short* y6 = p.y6 ? p.y6 + ob * (p.y_compact == 1 ? 1 : p.y_compact == 2 ? 2 : 3) : nullptr;
+  unsigned short* y6 = p.y6 ? p.y6 + ob * (p.y_compact == 1 ? 1 : p.y_compact >= 2 ? 2 : 3) : nullptr;
   unsigned short* y6s = p.y6s ? p.y6s + ob * (p.y6s_h2 ? 2 : 3) : nullptr;
   // Each thread finishes G consecutive output channels of a row (G = 8: 16-byte plane / compact
   // stores; the epilogue's store issue, not its bytes, sets its pace), the same channels for every
@@ -449,6 +449,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
         if (y6) {
           if (p.y_compact == 1) store_bf16x8(y6, orow, p.Cout, co, xv);
           else if (p.y_compact == 2) store_hm8(y6, orow, p.Cout, co, xv);
+          else if (p.y_compact == 3) store_h2_8(y6, orow, p.Cout, co, xv);
           else store_planes8(y6, orow, p.Cout, co, xv);
         }
         if (p.y2 || y6s) {
@@ -468,6 +469,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
         if (y6) {
           if (p.y_compact == 1) store_bf16x4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
           else if (p.y_compact == 2) store_hm4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
+          else if (p.y_compact == 3) store_h2_4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
           else store_planes4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
         }
         if (p.y2 || y6s) {
@@ -547,9 +549,10 @@ __device__ __forceinline__ void splitk_epi4(const ConvParams& p, const float* __
   }
   if (p.y) *reinterpret_cast<f32x4*>(p.y + o) = x;
   if (p.y6) {
-    unsigned short* y6 = p.y6 + ob * (p.y_compact == 1 ? 1 : p.y_compact == 2 ? 2 : 3);
+    unsigned short* y6 = p.y6 + ob * (p.y_compact == 1 ? 1 : p.y_compact >= 2 ? 2 : 3);
     if (p.y_compact == 1) store_bf16x4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
     else if (p.y_compact == 2) store_hm4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
+    else if (p.y_compact == 3) store_h2_4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
     else store_planes4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
   }
   if (p.y2 || p.y6s) {
@@ -2323,13 +2326,12 @@ static hipError_t launch_x6dq(const ConvParams& p, int batch, int phases, hipStr
 // scaled back by 2^-w3_shift before the epilogue.  A product keeps three terms, hh' + hl' + lh'
 // (ll' is 2^-22 relative), against x6's six, at the same K32 rate per MFMA
 // (v_mfma_f32_16x16x32_f16; the K16 f16 MFMA issues at half rate on gfx950, tools/probe).
-// A step is one 32-channel chunk of one tap; per 16 x 16 block three MFMAs, with the lane's
-// K group kg = lane >> 4 = (t, hf) = (lane >> 5, (lane >> 4) & 1):
-//   S1: A{h, group kg} . B{h', group kg}                                  = hh'
-//   S2: A{t ? l : h, group hf} . B{t ? h' : l', group hf}                 = hl' + lh' (groups 0, 1)
-//   S3: the same for groups 2 + hf                                        = hl' + lh' (groups 2, 3)
+// A step is one 32-channel chunk of one tap; per 16 x 16 block three MFMAs, A{h} . B{l'},
+// A{l} . B{h'} and A{h} . B{h'}, the lanes of K group kg = lane >> 4 holding channel group kg
+// (8 channels) of every operand, so a lane reads h and l of its rows and h' and l' of its columns
+// once per step.
 // Tiles BM x BN = 128 x 256 (BN = 256) or 256 x 128, 8 waves of 64 x 64 (group 0 the upper half of
-// the rows); every fragment of a step (12 A + 12 B ds_read_b128) is read in the memory segment and
+// the rows); every fragment of a step (8 A + 8 B ds_read_b128) is read in the memory segment and
 // an MFMA segment is 48 MFMAs.  LDS images, piece-major and row-linear: A [piece 8][BM + 64][16 B]
 // (two buffers, by chunk parity), B [piece 8][BN][16 B] (3-slot ring), piece = plane * 4 + channel
 // group; one 1 KiB DMA instruction fills 64 rows of one piece.  Rows of one piece are 16 B apart,
@@ -2338,16 +2340,19 @@ static hipError_t launch_x6dq(const ConvParams& p, int batch, int phases, hipStr
 // ---------------------------------------------------------------------------------------------
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-template <int BN>
+// HALO = 64: convs with a tap halo (taps >= 3), input chunks double-buffered by chunk parity;
+// HALO = 0 (conv_gemm_x3dm): one-tap convs, every step opens a chunk, so the input tiles ride the
+// weight ring's 3 slots, over a descriptor of the tile's rows only (32-bit offsets at any length).
+template <int BN, int HALO>
 __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, const int b, const int ph) {
-  constexpr int HALO = 64;
   constexpr int BM = 32768 / BN, WN = BN / 64, WM = 8 / WN;
+  constexpr int NA = HALO ? 2 : 3;
   constexpr int WR = BM / WM, WC = BN / WN, TM = WR / 16, TN = WC / 16;
   constexpr int AR = BM + HALO;                 // rows of an input image
   constexpr int A_G = AR / 16, B_G = BN / 16;   // 1 KiB DMA instructions per group (A per chunk, B per step)
   constexpr int A_PW = A_G / 4, B_PW = B_G / 4;
   constexpr int ABUF = AR * 128, BBUF = BN * 128;  // bytes
-  constexpr int LDS_B = 2 * ABUF + 3 * BBUF;
+  constexpr int LDS_B = NA * ABUF + 3 * BBUF;
   static_assert(WR == 64 && WC == 64 && A_G % 4 == 0 && B_G % 4 == 0 && AR % 64 == 0, "tile shape");
   static_assert(LDS_B <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) unsigned short lds[LDS_B / 2];
@@ -2365,8 +2370,11 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, con
   const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
   const int row0 = q0 + p.in_base[ph] + lo_rel;
   const int arow = p.ldx * 4;  // bytes per h2 row
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.x6 + (long long)b * p.x_bstride * 2), 0, p.Lin * arow, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx =
+      HALO ? __builtin_amdgcn_make_buffer_rsrc((void*)(p.x6 + (long long)b * p.x_bstride * 2), 0, p.Lin * arow, 0x00020000)
+           : __builtin_amdgcn_make_buffer_rsrc((void*)(p.x6 + ((long long)b * p.x_bstride + (long long)row0 * p.ldx) * 2), 0,
+                                               max(0, min(BM, p.Lin - row0)) * arow, 0x00020000);
+  const int rbase = HALO ? row0 : 0;  // row of image row 0 relative to the descriptor
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.w3 + (long long)ph * taps * nchunks * p.Cout * 64), 0, taps * nchunks * p.Cout * 128, 0x00020000);
 
@@ -2377,7 +2385,7 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, con
   for (int i = 0; i < A_PW; ++i) {
     const int u = (group * A_G + i * 4 + gw) * 64;
     const int pc = u / AR, row = u - pc * AR + lane;
-    a_off[i] = (row0 + row) * arow + (pc & 3) * 32 + (pc >> 2) * 16;  // negative rows: out of range
+    a_off[i] = (rbase + row) * arow + (pc & 3) * 32 + (pc >> 2) * 16;  // negative rows: out of range
   }
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
@@ -2386,12 +2394,13 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, con
     b_off[i] = (co0 + col) * 128 + (pc & 3) * 32 + (pc >> 2) * 16;
   }
   unsigned short* const a_dst = lds + (group * A_G + gw) * 512;
-  unsigned short* const b_dst = lds + ABUF + (group * B_G + gw) * 512;  // ushorts: 2 * ABUF bytes
+  unsigned short* const b_dst = lds + NA * ABUF / 2 + (group * B_G + gw) * 512;
   auto dma_step = [&](int c, int m, int slot) {
     int n = B_PW;
     if (m == 0) {
 #pragma unroll
-      for (int i = 0; i < A_PW; ++i) dma16(rx, a_dst + (c & 1) * (ABUF / 2) + i * 2048, a_off[i] + c * 128, 0);
+      for (int i = 0; i < A_PW; ++i)
+        dma16(rx, a_dst + (HALO ? (c & 1) : slot) * (ABUF / 2) + i * 2048, a_off[i] + c * 128, 0);
       n += A_PW;
     }
     const int soff = (m * nchunks + c) * p.Cout * 128;
@@ -2400,27 +2409,25 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, con
     return n;
   };
 
-  const int l15 = lane & 15, hf = (lane >> 4) & 1, t = lane >> 5, kg = lane >> 4;
-  // piece offsets (bytes) of the lane's three operand sets
-  const int pa0 = kg * AR * 16, pa1 = (t * 4 + hf) * AR * 16, pa2 = (t * 4 + 2 + hf) * AR * 16;
-  const int pb0 = kg * BN * 16, pb1 = ((1 - t) * 4 + hf) * BN * 16, pb2 = ((1 - t) * 4 + 2 + hf) * BN * 16;
+  const int l15 = lane & 15, kg = lane >> 4;
+  // piece offsets (bytes): h and l of the lane's channel group
+  const int pah = kg * AR * 16, pal = (4 + kg) * AR * 16;
+  const int pbh = kg * BN * 16, pbl = (4 + kg) * BN * 16;
   const char* const ldsb = reinterpret_cast<const char*>(lds);
-  const int bcol = 2 * ABUF + (wn * WC + l15) * 16;
-  s16x8 aq[TM][3], bq[TN][3];
+  const int bcol = NA * ABUF + (wn * WC + l15) * 16;
+  s16x8 aq[TM][2], bq[TN][2];  // [h, l]
   auto readF = [&](int c, int m, int slot) {
-    const char* a = ldsb + (c & 1) * ABUF + (wm * WR + m * p.in_step - lo_rel + l15) * 16;
+    const char* a = ldsb + (HALO ? (c & 1) : slot) * ABUF + (wm * WR + m * p.in_step - lo_rel + l15) * 16;
     const char* bb = ldsb + bcol + slot * BBUF;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      bq[j][0] = *reinterpret_cast<const s16x8*>(bb + j * 256 + pb0);
-      bq[j][1] = *reinterpret_cast<const s16x8*>(bb + j * 256 + pb1);
-      bq[j][2] = *reinterpret_cast<const s16x8*>(bb + j * 256 + pb2);
+      bq[j][0] = *reinterpret_cast<const s16x8*>(bb + j * 256 + pbh);
+      bq[j][1] = *reinterpret_cast<const s16x8*>(bb + j * 256 + pbl);
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      aq[i][0] = *reinterpret_cast<const s16x8*>(a + i * 256 + pa0);
-      aq[i][1] = *reinterpret_cast<const s16x8*>(a + i * 256 + pa1);
-      aq[i][2] = *reinterpret_cast<const s16x8*>(a + i * 256 + pa2);
+      aq[i][0] = *reinterpret_cast<const s16x8*>(a + i * 256 + pah);
+      aq[i][1] = *reinterpret_cast<const s16x8*>(a + i * 256 + pal);
     }
   };
   f32x4 acc[TM][TN];
@@ -2428,18 +2435,19 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, con
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // the cross terms first (S2, S3), then hh'; 16 independent accumulators between dependent MFMAs
+  // the cross terms first (hl', lh'), then hh'; 16 independent accumulators between dependent MFMAs
+  // (priority 1 while issuing MFMAs: without it the C2 step took 212.0 against 192.8 ms, r05k)
   auto mfma = [&]() {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const int set = k == 2 ? 0 : k + 1;
+      const int sa = k == 1 ? 1 : 0, sb = k == 0 ? 1 : 0;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, aq[i][set]),
-                                                             __builtin_bit_cast(f16x8, bq[j][set]), acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, aq[i][sa]),
+                                                             __builtin_bit_cast(f16x8, bq[j][sb]), acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
   };
@@ -2456,19 +2464,33 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, con
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   seg_barrier();
   int cr = 0, mr = 0;
+#ifdef DCX_SEG_DIAG
+  unsigned long long sd[6] = {};
+#endif
   if (group == 0) {
     readF(0, 0, 0);
     adv(cr, mr);
     int rs = 1, ws = 0;  // slot of the step read next (s + 1), of the step issued next (s + 3)
     for (int s = 0; s < nsteps; ++s) {
+      DCX_SEGT(ta);
       mfma();  // MFMA(s)
+      DCX_SEGT(tb);
       seg_barrier();
-      // MEM0(s): fragments of step s + 1, issue step s + 3, retire step s + 2
-      if (s + 1 < nsteps) readF(cr, mr, rs);
+      DCX_SEGT(tc);
+      // MEM0(s): issue step s + 3, fragments of step s + 1, retire step s + 2 (the DMA first: the
+      // fragment reads' latency then hides behind the DMA issue, C2 192.8 -> 190.3 ms, r05k)
       int n = 0;
       if (s + 3 < nsteps) n = dma_step(cl, ml, ws);
+      DCX_SEGT(tr);
+      if (s + 1 < nsteps) readF(cr, mr, rs);
+      DCX_SEGT(tq);
       wait_dma(n);
+      DCX_SEGT(td);
       seg_barrier();
+      DCX_SEGT(te);
+#ifdef DCX_SEG_DIAG
+      sd[0] += tb - ta; sd[1] += tc - tb; sd[2] += td - tc; sd[3] += te - td; sd[4] += tr - tc; sd[5] += tq - tr;
+#endif
       adv(cr, mr);
       adv(cl, ml);
       inc3(rs);
@@ -2477,23 +2499,40 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, con
   } else {
     int rs = 0, ws = 0;  // slot of step s, of step s + 2
     for (int s = 0; s < nsteps; ++s) {
-      // MEM1(s): fragments of step s, issue step s + 2 (s >= 1), retire step s + 1
-      readF(cr, mr, rs);
+      DCX_SEGT(ta);
+      // MEM1(s): issue step s + 2 (s >= 1), fragments of step s, retire step s + 1
       int n = 0;
       if (s >= 1 && s + 2 < nsteps) {
         n = dma_step(cl, ml, ws);
         adv(cl, ml);
       }
+      DCX_SEGT(tr);
+      readF(cr, mr, rs);
+      DCX_SEGT(tq);
       wait_dma(n);
+      DCX_SEGT(tb);
       seg_barrier();
+      DCX_SEGT(tc);
       mfma();  // MFMA(s)
+      DCX_SEGT(td);
       seg_barrier();
+      DCX_SEGT(te);
+#ifdef DCX_SEG_DIAG
+      sd[2] += tb - ta; sd[3] += tc - tb; sd[0] += td - tc; sd[1] += te - td; sd[4] += tr - ta; sd[5] += tq - tr;
+#endif
       adv(cr, mr);
       inc3(rs);
       if (s >= 1) inc3(ws);
       else ws = 0;  // step 3's slot
     }
   }
+#ifdef DCX_SEG_DIAG
+  if ((threadIdx.x & 255) == 0) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) atomicAdd(&g_seg_diag[group * 6 + i], sd[i]);
+    if (group == 0) atomicAdd(&g_seg_diag[12], (unsigned long long)nsteps);
+  }
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // undo the weight scaling (a power of two: exact)
   const float unscale = __builtin_ldexpf(1.0f, -p.w3_shift);
@@ -2504,11 +2543,11 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, con
   epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
-template <int BN>
+template <int BN, int HALO>
 __global__ void __launch_bounds__(512, 2) conv_gemm_x3dq(const ConvParams p) {
   int wg, b, ph;
   flat_tile(((p.Lq + 32768 / BN - 1) / (32768 / BN)) * (p.Cout / BN), p.batch, wg, b, ph);
-  x3dq_tile<BN>(p, wg, b, ph);
+  x3dq_tile<BN, HALO>(p, wg, b, ph);
 }
 
 // grouped launch of up to 3 h3 convs (conv_gemm_x6dq_group's member mapping)
@@ -2522,19 +2561,27 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x3dq_group(const ConvGroup g
   if (k == 0) p = g.p[0];
   else if (k == 1) p = g.p[1];
   else p = g.p[2];
-  x3dq_tile<BN>(p, local - b * g.tiles_per_clip[k], b, 0);
+  x3dq_tile<BN, 64>(p, local - b * g.tiles_per_clip[k], b, 0);
 }
 
-// Whether conv_gemm_x3dq<bn> takes an h3 conv (input in the h2 layout, x_compact == 3).
+// Whether conv_gemm_x3dq<bn> (taps >= 3 with a halo) or conv_gemm_x3dm<bn> (one tap) takes an h3
+// conv (input in the h2 layout, x_compact == 3).
 static bool x3dq_ok(const ConvParams& p, int bn) {
   const int span = (p.taps - 1) * (p.in_step < 0 ? -p.in_step : p.in_step);
-  if (!p.x6 || !p.w3 || p.x_compact != 3 || p.Cin % 32 || p.Cout % bn || p.taps < 3 || span == 0 || span > 64 ||
-      p.ksplit > 1)
-    return false;
+  if (!p.x6 || !p.w3 || p.x_compact != 3 || p.Cin % 32 || p.Cout % bn || p.ksplit > 1) return false;
   const long long arow = (long long)p.ldx * 4;
-  return (long long)(p.Lin + 1024) * arow < (1LL << 31) && (long long)p.taps * p.Cin * p.Cout * 4 < (1LL << 31);
+  if ((long long)p.taps * p.Cin * p.Cout * 4 >= (1LL << 31)) return false;
+  if (p.taps == 1) {  // per-tile descriptor: every phase's rows start at or after the tile's
+    for (int i = 0; i < kMaxPhases; ++i)
+      if (p.in_base[i] < 0) return false;
+    return 256LL * arow < (1LL << 31);
+  }
+  return p.taps >= 3 && span > 0 && span <= 64 && (long long)(p.Lin + 1024) * arow < (1LL << 31);
 }
-static int x3dq_bn(const ConvParams& p) { return p.Cout % 256 == 0 ? 256 : 128; }
+// 256 x 128 tiles: against 128 x 256 they halve the weight DMA per step (A: 40 KiB per chunk, B
+// 16 KiB per step, against 24 and 32), C2 205.1 -> 193.2 ms (r05i).  Knobs::h3_bn = 256
+// (DCX_H3_BN=256): the 128 x 256 tiles at Cout % 256 == 0 (A/B).
+static int x3dq_bn(const ConvParams& p) { return p.Cout % 256 == 0 && p.kn && p.kn->h3_bn == 256 ? 256 : 128; }
 
 // ---------------------------------------------------------------------------------------------
 // conv_gemm_bf16dm: the DCX_GEMM_BF16 mode's 1x1 convs (one hi * hi' product, the reference's
@@ -4064,8 +4111,13 @@ static hipError_t launch_x3dq(const ConvParams& p, int batch, int phases, hipStr
   ConvParams q = p;
   q.batch = batch;
   q.phases = phases;
-  if (kname) *kname = BN == 256 ? "conv_gemm_x3dq<128,256,halo>" : "conv_gemm_x3dq<256,128,halo>";
-  hipLaunchKernelGGL((conv_gemm_x3dq<BN>), grid, dim3(512), 0, s, q);
+  if (p.taps == 1) {
+    if (kname) *kname = BN == 256 ? "conv_gemm_x3dm<128,256>" : "conv_gemm_x3dm<256,128>";
+    hipLaunchKernelGGL((conv_gemm_x3dq<BN, 0>), grid, dim3(512), 0, s, q);
+  } else {
+    if (kname) *kname = BN == 256 ? "conv_gemm_x3dq<128,256,halo>" : "conv_gemm_x3dq<256,128,halo>";
+    hipLaunchKernelGGL((conv_gemm_x3dq<BN, 64>), grid, dim3(512), 0, s, q);
+  }
   return hipGetLastError();
 }
 
@@ -4204,7 +4256,7 @@ hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t
   if (ps[0].x_compact == 3) {  // h3 convs: conv_gemm_x3dq_group (any tile count)
     const int bn = x3dq_bn(ps[0]), bm = 32768 / bn;
     for (int i = 0; i < n; ++i)
-      if (ps[i].Cout != cout || ps[i].x_compact != 3 || !x3dq_ok(ps[i], bn)) return hipErrorNotSupported;
+      if (ps[i].Cout != cout || ps[i].x_compact != 3 || ps[i].taps < 3 || !x3dq_ok(ps[i], bn)) return hipErrorNotSupported;
     int order[kMaxGroup] = {0, 1, 2};
     for (int i = 0; i < n; ++i)
       for (int j = i + 1; j < n; ++j)

@@ -36,7 +36,9 @@ struct Knobs {
   int dwconv_tiled = 0;     // DCX_DWCONV_TILED=1: the round-2 tiled dwconv_ln (same bits)
   int split_min_steps = 0;  // DCX_SPLIT_MIN_STEPS: split-K only convs with at least this many K steps
   int split_group_off = 0;  // DCX_SPLIT_GROUP_OFF=1: per-conv split launches instead of grouped ones
-  int h3 = 0;               // DCX_H3=1: the wide generator stages' ResBlock convs in h3 arithmetic (x6 mode)
+  int h3 = 1;               // DCX_H3=0: the wide generator stages' ResBlock convs in x6 arithmetic (A/B, tests)
+  int h3_bn = 0;            // DCX_H3_BN=256: conv_gemm_x3dq's 128 x 256 tiles at Cout % 256 == 0 (A/B)
+  int h3_1x1 = 1;           // DCX_H3_1X1=0: the ConvNeXt blocks' 1x1 convs in x6 arithmetic (A/B, tests)
 };
 
 // out[b][q*out_mul + phase][co] = epi( sum_{m<taps} sum_{ci<Cin} x[b][q + in_base[phase] + m*in_step][ci]

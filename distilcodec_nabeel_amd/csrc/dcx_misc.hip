@@ -63,7 +63,8 @@ __device__ __forceinline__ void ln_finish(f32x4 (&v)[NV], int C, float eps, int 
     }
     if (yrow) *reinterpret_cast<f32x4*>(yrow + c) = o;
     if (y6) {
-      if (y6c) store_bf16x4(y6, row, C, c, o.x, o.y, o.z, o.w);
+      if (y6c == 1) store_bf16x4(y6, row, C, c, o.x, o.y, o.z, o.w);
+      else if (y6c == 3) store_h2_4(y6, row, C, c, o.x, o.y, o.z, o.w);  // h3 input (conv_gemm_x3dm)
       else store_planes4(y6, row, C, c, o.x, o.y, o.z, o.w);
     }
   }

@@ -1,4 +1,4 @@
-"""The h3 arithmetic of the wide generator stages (Knobs::h3, DCX_H3=1; conv_gemm_x3dq).
+"""The h3 arithmetic of the wide generator stages (Knobs::h3, the default; DCX_H3=0 gives x6).
 
 The ResBlock convs of the C = 512 / 256 / 128 stages take their inputs as two fp16 values
 (h = fp16(x), l = fp16(x - h): 22 significant bits) and the weights likewise after a power-of-two
@@ -47,7 +47,8 @@ def test_parallel_block_h3_vs_oracle(eng, state, cfg, stage):
     x = torch.from_numpy(np.random.default_rng(10 + stage).standard_normal((2, C, 300)).astype(np.float32))
     ref = torch.nn.functional.silu(R.parallel_block(x.double(), state["generator"], stage, cfg["decoder"], torch.float64))
     ref = ref.numpy()
-    y6 = eng.module(f"generator.resblocks.{stage}", _cl(x.numpy())).cpu().numpy().transpose(0, 2, 1)
+    with eng.knobs(DCX_H3=0):
+        y6 = eng.module(f"generator.resblocks.{stage}", _cl(x.numpy())).cpu().numpy().transpose(0, 2, 1)
     with eng.knobs(DCX_H3=1):
         y3 = eng.module(f"generator.resblocks.{stage}", _cl(x.numpy())).cpu().numpy().transpose(0, 2, 1)
     e6, e3 = _rel(y6, ref), _rel(y3, ref)
@@ -75,21 +76,60 @@ def test_generator_h3_vs_x6(eng, golden):
     for name in ("e2e_batch", "e2e_real"):
         g = golden[name]
         z = torch.from_numpy(g["quantized"]).transpose(1, 2)
-        w6 = eng.generate(z).cpu().numpy()
-        with eng.knobs(DCX_H3=1):
-            w3 = eng.generate(z).cpu().numpy()
+        with eng.knobs(DCX_H3=0):
+            w6 = eng.generate(z).cpu().numpy()
+        w3 = eng.generate(z).cpu().numpy()
         s36, s3r = _snr(w3, w6), _snr(w3, g["wav"])
         print(f"\n{name}: h3 vs x6 {s36:.1f} dB, h3 vs reference {s3r:.1f} dB (x6 vs reference {_snr(w6, g['wav']):.1f})")
         assert s36 >= 100, (name, s36)
         assert s3r >= 80, (name, s3r)
 
 
-def test_h3_knob_off_is_x6_bits(eng, golden):
-    """The knob switches kernels only where it says: off again gives the x6 path's bits."""
+def test_h3_knob_switches_back(eng, golden):
+    """The knob switches kernels only where it says: x6, h3, x6 again gives the first bits, and h3
+    runs are reproducible."""
     g = golden["e2e_3s"]
     z = torch.from_numpy(g["quantized"]).transpose(1, 2)
-    a = eng.generate(z).cpu().numpy()
-    with eng.knobs(DCX_H3=1):
-        eng.generate(z)
-    b = eng.generate(z).cpu().numpy()
+    with eng.knobs(DCX_H3=0):
+        a = eng.generate(z).cpu().numpy()
+    c = eng.generate(z).cpu().numpy()
+    with eng.knobs(DCX_H3=0):
+        b = eng.generate(z).cpu().numpy()
     assert np.array_equal(a, b)
+    assert np.array_equal(c, eng.generate(z).cpu().numpy())
+    assert not np.array_equal(a, c)
+
+
+@pytest.mark.parametrize("bn", [0, 256])
+def test_tilings_agree(eng, state, cfg, bn):
+    """The 256 x 128 (default) and 128 x 256 tilings sum every output in the same order: same bits."""
+    C = cfg["decoder"]["upsample_initial_channel"] >> 1
+    x = torch.from_numpy(np.random.default_rng(5).standard_normal((1, C, 700)).astype(np.float32))
+    ref = eng.module("generator.resblocks.0", _cl(x.numpy())).cpu().numpy()
+    with eng.knobs(DCX_H3_BN=bn):
+        y = eng.module("generator.resblocks.0", _cl(x.numpy())).cpu().numpy()
+    assert np.array_equal(y, ref)
+
+
+def test_encoder_h3_vs_x6(eng, golden):
+    """The ConvNeXt blocks' 1x1 convs (conv_gemm_x3dm, Knobs::h3_1x1): encoder features against
+    the reference within the x6 bound, and within 4x of the x6 path's own error."""
+    g = golden["e2e_batch"]
+    mel = torch.from_numpy(g["mel"]).transpose(1, 2)
+    with eng.knobs(DCX_H3_1X1=0):
+        f6 = eng.encode(mel).transpose(1, 2).cpu().numpy()
+    f3 = eng.encode(mel).transpose(1, 2).cpu().numpy()
+    e6, e3 = _rel(f6, g["feat"]), _rel(f3, g["feat"])
+    print(f"\nencoder rel err: x6 {e6:.3g}, h3 {e3:.3g}")
+    assert e3 < 2e-4
+    assert e3 < 4 * max(e6, 1e-7)
+
+
+def test_convnext_block_h3_vs_oracle(eng, golden, state):
+    m = golden["modules"]
+    x = _cl(m["convnext256_in"])
+    with eng.knobs(DCX_H3_1X1=0):
+        y6 = eng.module("encoder.stages.0.0", x).transpose(1, 2).cpu().numpy()
+    y3 = eng.module("encoder.stages.0.0", x).transpose(1, 2).cpu().numpy()
+    assert _rel(y3, m["convnext256_out"]) < 2e-4
+    assert not np.array_equal(y3, y6)  # the h3 path ran

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Per-segment cycle breakdown of conv_gemm_x3dq's ping-pong main loop (library built with
+-DDCX_SEG_DIAG, exporting dcx_diag_seg; select it with DCX_LIB=...), on the ResBlock convs of the
+wide generator stages in h3 arithmetic (DCX_H3=1).
+
+    DCX_LIB=$PWD/distilcodec_nabeel_amd/libdcx_seg.so python tools/seg_diag_h3.py [--stages 0,1,2]
+
+Per K32 step and per wave (group 0 / group 1): cycles issuing the MFMAs, waiting at the barrier
+after them, in the memory segment (DMA issue, fragment reads, the counted DMA wait; the first two
+also shown apart), and waiting at the barrier after it.  Averages over every tile of every conv of the stage's ParallelBlock.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distilcodec_nabeel_amd import _native, config, weights  # noqa: E402
+from distilcodec_nabeel_amd.engine import NativeCodec  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stages", default="0,1,2")
+    ap.add_argument("--rows", type=int, default=19200, help="rows (B * L) of the stage input")
+    a = ap.parse_args()
+    cfg = config.default_config()
+    eng = NativeCodec(cfg, weights.synthetic_state_dict(cfg, seed=1), "cuda:0", gemm="x6")
+    eng.set_knob("DCX_H3", 1)
+    f = _native.lib().dcx_diag_seg
+    f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    for st in [int(s) for s in a.stages.split(",")]:
+        C = cfg["decoder"]["upsample_initial_channel"] >> (st + 1)
+        x = torch.randn(4, a.rows // 4, C, device="cuda")
+        eng.module(f"generator.resblocks.{st}", x)
+        torch.cuda.synchronize()
+        out = (ctypes.c_ulonglong * 13)()
+        f(out, 1)
+        for _ in range(3):
+            eng.module(f"generator.resblocks.{st}", x)
+        torch.cuda.synchronize()
+        f(out, 1)
+        n = max(out[12], 1)
+        v = [out[i] / n for i in range(12)]
+        lab = ["mfma", "wait", "mem", "wait", "(dma issue", "reads"]
+        for g in range(2):
+            print(f"stage {st} (C = {C}) g{g}: " + "  ".join(f"{lab[i]} {v[6 * g + i]:6.0f}" for i in range(6))
+                  + f")  | step {sum(v[6 * g:6 * g + 4]):6.0f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
