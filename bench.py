@@ -53,6 +53,8 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (= 
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 # x6 mode executes 6 exact bf16 products per fp32 product: its ceiling in fp32-algorithmic FLOP/s
 X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
+# h3 (the wide convs since round 5): 3 exact fp16 products per fp32 product, fp16 MFMA at the bf16 rate
+H3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
 HBM_PEAK_GBS = 8000.0
 SR = 24000
 MFLOP_PER_FRAME = 2045.08  # encode -> decode algorithmic work per 256-sample frame
@@ -297,12 +299,13 @@ def roofline(prof: dict, steps: int):
     name, rec = max(prof.items(), key=lambda kv: kv[1]["ms"])
     avg_ms = rec["ms"] / rec["launches"]
     achieved = rec["flops"] / (rec["ms"] * 1e-3) / 1e12
-    peak = X6_PEAK_TFLOPS if "x6" in name else FP32_MFMA_PEAK_TFLOPS
+    peak = H3_PEAK_TFLOPS if "x3" in name else X6_PEAK_TFLOPS if "x6" in name else FP32_MFMA_PEAK_TFLOPS
     return {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": round(peak, 1),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic_for(name),
             "traffic_source": "committed PMC figure (profiles/pmc_latest.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                               "passes over bench.py, 2*FETCH + WRITE per launch), not measured in this run",
-            "peak_basis": ("bf16 dense MFMA 2500 TF / 6 bf16 products per fp32 product" if "x6" in name
+            "peak_basis": ("dense fp16 MFMA 2500 TF / 3 fp16 products per fp32 product (h3)" if "x3" in name
+                           else "bf16 dense MFMA 2500 TF / 6 bf16 products per fp32 product" if "x6" in name
                            else "fp32 MFMA v_mfma_f32_32x32x2_f32"),
             "launches_per_step": rec["launches"] // steps, "avg_launch_ms": round(avg_ms, 4),
             "flops_per_launch": rec["flops"] / rec["launches"],

@@ -2395,7 +2395,11 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, con
   }
   unsigned short* const a_dst = lds + (group * A_G + gw) * 512;
   unsigned short* const b_dst = lds + NA * ABUF / 2 + (group * B_G + gw) * 512;
+  [[maybe_unused]] bool in_loop = false;  // -DDCX_X3_NODMA (diagnostic): no DMA after the prologue (wrong results)
   auto dma_step = [&](int c, int m, int slot) {
+#ifdef DCX_X3_NODMA
+    if (in_loop) return 0;
+#endif
     int n = B_PW;
     if (m == 0) {
 #pragma unroll
@@ -2463,6 +2467,7 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, con
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   seg_barrier();
+  in_loop = true;
   int cr = 0, mr = 0;
 #ifdef DCX_SEG_DIAG
   unsigned long long sd[6] = {};
@@ -2564,6 +2569,230 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x3dq_group(const ConvGroup g
   x3dq_tile<BN, 64>(p, local - b * g.tiles_per_clip[k], b, 0);
 }
 
+// ---------------------------------------------------------------------------------------------
+// conv_gemm_x3dw: h3 arithmetic on 256 x 256 tiles (64 x 128 wave tiles, 96 MFMAs per segment).
+//
+// Segment stamps of x3dq / x3dm (tools/seg_diag_h3.py) put their memory segment, and within it the
+// DMA issue, at or above the MFMA segment: a CU takes in about 16 B per cycle by LDS-DMA, and a
+// 256 x 128 tile needs (A / taps + B) bytes per 48 MFMAs per wave.  A 256 x 256 tile moves the same
+// A and twice the columns per step, and a 64 x 128 wave tile issues twice the MFMAs per fragment
+// read.  It fits the LDS with a 2-slot step ring (B 32 KiB per slot; A 40 KiB per chunk, double-
+// buffered by chunk parity, or, one-tap, 32 KiB riding the B slot): 144 / 128 KiB.
+// Schedule (segment 2s = MFMA0(s) | MEM1(s), 2s + 1 = MEM0(s) | MFMA1(s); step t in slot t % 2):
+//   * group 1 reads step s in MEM1(s); group 0 reads step s + 1 in MEM0(s);
+//   * group 0 alone issues the DMA: step s + 2 in MEM0(s) (step s's slot, whose last reader was
+//     MEM1(s)), and waits for it (vmcnt(0)) at the end of MFMA0(s + 1), before the barrier that
+//     opens MEM0(s + 1), its first reader: one segment of MFMAs covers the DMA latency.
+//   * A chunk c (halo) is issued with step c * taps into buffer c & 1, whose last reader (chunk
+//     c - 2's last step, MEM1((c - 1) * taps - 1)) is at least two segments earlier for taps >= 2.
+// Per-lane DMA offsets are one VGPR per operand (row base) plus a wave-uniform add per piece.
+// ---------------------------------------------------------------------------------------------
+template <int HALO>
+__device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, const int b, const int ph) {
+  constexpr int BM = 256, BN = 256, WN = 2, WM = 4;
+  constexpr int WR = 64, WC = 128, TM = 4, TN = 8;
+  constexpr int AR = BM + HALO;                 // rows of an input image
+  constexpr int A_N = AR / 8, B_N = BN / 8;     // 1 KiB DMA instructions per A chunk / B step
+  constexpr int A_PW = A_N / 4, B_PW = B_N / 4; // per group-0 wave
+  constexpr int ABUF = AR * 128, BBUF = BN * 128;  // bytes
+  constexpr int NA = 2;                         // A buffers (halo: chunk parity; one tap: step slot)
+  constexpr int LDS_B = NA * ABUF + 2 * BBUF;
+  static_assert(A_N % 4 == 0 && B_N % 4 == 0 && AR % 64 == 0, "tile shape");
+  static_assert(LDS_B <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned short lds[LDS_B / 2];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int group = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int wm = wave / WN, wn = wave % WN;
+  const int ntiles = p.Cout / BN;
+  const int mt = wg / ntiles, nt = wg - mt * ntiles;
+  const int q0 = mt * BM, co0 = nt * BN;
+  const int nchunks = p.Cin / 32;
+  const int taps = p.taps;
+  const int nsteps = nchunks * taps;
+  const int lo_rel = p.in_step < 0 ? (taps - 1) * p.in_step : 0;
+  const int row0 = q0 + p.in_base[ph] + lo_rel;
+  const int arow = p.ldx * 4;  // bytes per h2 row
+  const __amdgpu_buffer_rsrc_t rx =
+      HALO ? __builtin_amdgcn_make_buffer_rsrc((void*)(p.x6 + (long long)b * p.x_bstride * 2), 0, p.Lin * arow, 0x00020000)
+           : __builtin_amdgcn_make_buffer_rsrc((void*)(p.x6 + ((long long)b * p.x_bstride + (long long)row0 * p.ldx) * 2), 0,
+                                               max(0, min(BM, p.Lin - row0)) * arow, 0x00020000);
+  const int rbase = HALO ? row0 : 0;  // row of image row 0 relative to the descriptor
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.w3 + (long long)ph * taps * nchunks * p.Cout * 64), 0, taps * nchunks * p.Cout * 128, 0x00020000);
+
+  // DMA (group 0 alone): instruction k fills 64 rows of piece (k * 64) / rows; the wave's i-th is
+  // k = i * 4 + gw.  Lane part of the source offset in one VGPR, the rest wave-uniform.  (Group 1
+  // issuing half of the weight pieces from inside its MFMA segment, so that the DMA of a step is in
+  // flight in both segments, measured slower: C2 194.2-194.7 against 185.3-185.4 ms, r05n; the
+  // issue stalls behind group 0's and holds up the MFMAs.)
+  const int a_lane = (rbase + lane) * arow;  // negative rows: huge unsigned, out of range (zeros)
+  const int b_lane = (co0 + lane) * 128;
+  [[maybe_unused]] bool in_loop = false;  // -DDCX_X3_NODMA (diagnostic): no DMA after the prologue (wrong results)
+  auto dmaA1 = [&](int c, int slot, int i) {  // the wave's i-th A piece of chunk c
+#ifdef DCX_X3_NODMA
+    if (in_loop) return;
+#endif
+    const int k = i * 4 + gw;
+    const int u = k * 64, pc = u / AR, row = u - pc * AR;
+    const int abuf = HALO ? (c & 1) : slot;
+    dma16(rx, lds + abuf * (ABUF / 2) + k * 512, a_lane + row * arow + (pc & 3) * 32 + (pc >> 2) * 16 + c * 128, 0);
+  };
+  auto dmaB1 = [&](int c, int m, int slot, int i) {  // the wave's i-th B piece of step (c, m)
+#ifdef DCX_X3_NODMA
+    if (in_loop) return;
+#endif
+    const int k = i * 4 + gw;
+    const int u = k * 64, pc = u / BN, col = u - pc * BN;
+    dma16(rw, lds + NA * ABUF / 2 + slot * (BBUF / 2) + k * 512, b_lane + col * 128 + (pc & 3) * 32 + (pc >> 2) * 16,
+          (m * nchunks + c) * p.Cout * 128);
+  };
+  auto dma_step = [&](int c, int m, int slot) {  // a step's pieces (its input chunk first when it opens one)
+    if (m == 0) {
+#pragma unroll
+      for (int i = 0; i < A_PW; ++i) dmaA1(c, slot, i);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) dmaB1(c, m, slot, i);
+  };
+
+  // fragment addresses: one lane base per operand (h piece of the lane's channel group kg); the
+  // l piece, row / column blocks and the B slot are immediate offsets
+  const int l15 = lane & 15, kg = lane >> 4;
+  const char* const ldsb = reinterpret_cast<const char*>(lds);
+  const char* const a_rd = ldsb + kg * AR * 16 + (wm * WR + l15) * 16;
+  const char* const b_rd = ldsb + NA * ABUF + kg * BN * 16 + (wn * WC + l15) * 16;
+  s16x8 aq[TM][2], bq[TN][2];  // [h, l]
+  auto readF = [&](int c, int m, int slot) {
+    const char* a = a_rd + ((HALO ? (c & 1) : slot) * ABUF + (m * p.in_step - lo_rel) * 16);
+    const char* bb = b_rd + slot * BBUF;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bq[j][0] = *reinterpret_cast<const s16x8*>(bb + j * 256);
+      bq[j][1] = *reinterpret_cast<const s16x8*>(bb + j * 256 + 4 * BN * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      aq[i][0] = *reinterpret_cast<const s16x8*>(a + i * 256);
+      aq[i][1] = *reinterpret_cast<const s16x8*>(a + i * 256 + 4 * AR * 16);
+    }
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int sa = k == 1 ? 1 : 0, sb = k == 0 ? 1 : 0;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, aq[i][sa]),
+                                                             __builtin_bit_cast(f16x8, bq[j][sb]), acc[i][j], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto adv = [&](int& c_, int& m_) {
+    if (++m_ == taps) { m_ = 0; ++c_; }
+  };
+
+  // prologue: steps 0 and 1 (group 0 issues), drained
+  int cl = 0, ml = 0;  // the next step group 0 issues
+  for (int t = 0; t < 2 && t < nsteps; ++t) {
+    if (group == 0) dma_step(cl, ml, t);
+    adv(cl, ml);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  seg_barrier();
+  in_loop = true;
+#ifdef DCX_SEG_DIAG
+  unsigned long long sd[6] = {};
+#endif
+  int cr = 0, mr = 0;
+  if (group == 0) {
+    readF(0, 0, 0);
+    adv(cr, mr);
+    for (int s = 0; s < nsteps; ++s) {
+      DCX_SEGT(ta);
+      mfma();  // MFMA(s)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step s + 1 (issued in MEM0(s - 1)) landed
+      DCX_SEGT(tb);
+      seg_barrier();
+      DCX_SEGT(tc);
+      // MEM0(s): issue step s + 2 into step s's slot, fragments of step s + 1
+      if (s + 2 < nsteps) {
+        dma_step(cl, ml, s & 1);
+        adv(cl, ml);
+      }
+      DCX_SEGT(tr);
+      if (s + 1 < nsteps) readF(cr, mr, (s + 1) & 1);
+      DCX_SEGT(tq);
+      DCX_SEGT(td);
+      seg_barrier();
+      DCX_SEGT(te);
+#ifdef DCX_SEG_DIAG
+      sd[0] += tb - ta; sd[1] += tc - tb; sd[2] += td - tc; sd[3] += te - td; sd[4] += tr - tc; sd[5] += tq - tr;
+#endif
+      adv(cr, mr);
+    }
+  } else {
+    for (int s = 0; s < nsteps; ++s) {
+      DCX_SEGT(ta);
+      readF(cr, mr, s & 1);  // MEM1(s): fragments of step s
+      DCX_SEGT(tb);
+      seg_barrier();
+      DCX_SEGT(tc);
+      mfma();  // MFMA(s)
+      DCX_SEGT(td);
+      seg_barrier();
+      DCX_SEGT(te);
+#ifdef DCX_SEG_DIAG
+      sd[2] += tb - ta; sd[3] += tc - tb; sd[0] += td - tc; sd[1] += te - td; sd[5] += tb - ta;
+#endif
+      adv(cr, mr);
+    }
+  }
+#ifdef DCX_SEG_DIAG
+  if ((threadIdx.x & 255) == 0) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) atomicAdd(&g_seg_diag[group * 6 + i], sd[i]);
+    if (group == 0) atomicAdd(&g_seg_diag[12], (unsigned long long)nsteps);
+  }
+#endif
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const float unscale = __builtin_ldexpf(1.0f, -p.w3_shift);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] *= unscale;
+  epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+}
+
+template <int HALO>
+__global__ void __launch_bounds__(512, 2) conv_gemm_x3dw(const ConvParams p) {
+  int wg, b, ph;
+  flat_tile(((p.Lq + 255) / 256) * (p.Cout / 256), p.batch, wg, b, ph);
+  x3dw_tile<HALO>(p, wg, b, ph);
+}
+
+__global__ void __launch_bounds__(512, 2) conv_gemm_x3dw_group(const ConvGroup g) {
+  const int t = blockIdx.x;
+  const int k = t >= g.start[1] ? (t >= g.start[2] ? 2 : 1) : 0;
+  const int local = xcd_remap(t - g.start[k], g.start[k + 1] - g.start[k]);
+  const int b = local / g.tiles_per_clip[k];
+  ConvParams p;
+  if (k == 0) p = g.p[0];
+  else if (k == 1) p = g.p[1];
+  else p = g.p[2];
+  x3dw_tile<64>(p, local - b * g.tiles_per_clip[k], b, 0);
+}
+
 // Whether conv_gemm_x3dq<bn> (taps >= 3 with a halo) or conv_gemm_x3dm<bn> (one tap) takes an h3
 // conv (input in the h2 layout, x_compact == 3).
 static bool x3dq_ok(const ConvParams& p, int bn) {
@@ -2578,10 +2807,15 @@ static bool x3dq_ok(const ConvParams& p, int bn) {
   }
   return p.taps >= 3 && span > 0 && span <= 64 && (long long)(p.Lin + 1024) * arow < (1LL << 31);
 }
-// 256 x 128 tiles: against 128 x 256 they halve the weight DMA per step (A: 40 KiB per chunk, B
-// 16 KiB per step, against 24 and 32), C2 205.1 -> 193.2 ms (r05i).  Knobs::h3_bn = 256
-// (DCX_H3_BN=256): the 128 x 256 tiles at Cout % 256 == 0 (A/B).
-static int x3dq_bn(const ConvParams& p) { return p.Cout % 256 == 0 && p.kn && p.kn->h3_bn == 256 ? 256 : 128; }
+// Tiles of an h3 conv: 256 x 256 (conv_gemm_x3dw) where Cout % 256 == 0, else 256 x 128.  (256 x 128
+// against 128 x 256: half the weight DMA per step, C2 205.1 -> 193.2 ms, r05i.)  Knobs::h3_bn
+// (DCX_H3_BN, A/B): 128 = the 256 x 128 tiles everywhere, 256 = the 128 x 256 ones at Cout % 256 == 0.
+// Returns the column tile, 512 standing for the 256 x 256 kernel.
+static int x3dq_bn(const ConvParams& p) {
+  const int k = p.kn ? p.kn->h3_bn : 0;
+  if (p.Cout % 256) return 128;
+  return k == 128 ? 128 : k == 256 ? 256 : 512;
+}
 
 // ---------------------------------------------------------------------------------------------
 // conv_gemm_bf16dm: the DCX_GEMM_BF16 mode's 1x1 convs (one hi * hi' product, the reference's
@@ -4125,7 +4359,21 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
   if (p.Cin % BK || p.Cout % 32 || phases < 1 || phases > kMaxPhases) return hipErrorInvalidValue;
   if (p.x_compact == 3) {  // h2 input: the h3 kernels only
     const int bn = x3dq_bn(p);
-    if (!x3dq_ok(p, bn)) return hipErrorInvalidValue;
+    if (!x3dq_ok(p, bn == 512 ? 256 : bn)) return hipErrorInvalidValue;
+    if (bn == 512) {
+      const dim3 grid((unsigned)(((p.Lq + 255) / 256) * (p.Cout / 256) * batch * phases));
+      ConvParams q = p;
+      q.batch = batch;
+      q.phases = phases;
+      if (p.taps == 1) {
+        if (kname) *kname = "conv_gemm_x3dw<256,256>";
+        hipLaunchKernelGGL((conv_gemm_x3dw<0>), grid, dim3(512), 0, s, q);
+      } else {
+        if (kname) *kname = "conv_gemm_x3dw<256,256,halo>";
+        hipLaunchKernelGGL((conv_gemm_x3dw<64>), grid, dim3(512), 0, s, q);
+      }
+      return hipGetLastError();
+    }
     return bn == 256 ? launch_x3dq<256>(p, batch, phases, s, kname) : launch_x3dq<128>(p, batch, phases, s, kname);
   }
   if (p.w6) {
@@ -4253,8 +4501,8 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
 hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t s, const char** kname) {
   if (n < 1 || n > kMaxGroup || batch < 1) return hipErrorInvalidValue;
   const int cout = ps[0].Cout;
-  if (ps[0].x_compact == 3) {  // h3 convs: conv_gemm_x3dq_group (any tile count)
-    const int bn = x3dq_bn(ps[0]), bm = 32768 / bn;
+  if (ps[0].x_compact == 3) {  // h3 convs: conv_gemm_x3dw_group / x3dq_group (any tile count)
+    const int bsel = x3dq_bn(ps[0]), bn = bsel == 512 ? 256 : bsel, bm = bsel == 512 ? 256 : 32768 / bn;
     for (int i = 0; i < n; ++i)
       if (ps[i].Cout != cout || ps[i].x_compact != 3 || ps[i].taps < 3 || !x3dq_ok(ps[i], bn)) return hipErrorNotSupported;
     int order[kMaxGroup] = {0, 1, 2};
@@ -4272,7 +4520,10 @@ hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t
     }
     if (start > (1LL << 30)) return hipErrorInvalidValue;
     for (int k = n; k <= kMaxGroup; ++k) g.start[k] = (int)start;
-    if (bn == 256) {
+    if (bsel == 512) {
+      if (kname) *kname = "conv_gemm_x3dw_group<256,256,halo>";
+      hipLaunchKernelGGL(conv_gemm_x3dw_group, dim3((unsigned)start), dim3(512), 0, s, g);
+    } else if (bn == 256) {
       if (kname) *kname = "conv_gemm_x3dq_group<128,256,halo>";
       hipLaunchKernelGGL((conv_gemm_x3dq_group<256>), dim3((unsigned)start), dim3(512), 0, s, g);
     } else {

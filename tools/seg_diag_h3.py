@@ -25,28 +25,45 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stages", default="0,1,2")
     ap.add_argument("--rows", type=int, default=19200, help="rows (B * L) of the stage input")
+    ap.add_argument("--blocks", default="", help="encoder ConvNeXt blocks instead (conv_gemm_x3dm), e.g. 0.0,2.0")
+    ap.add_argument("--no-diag", action="store_true", help="run the modules only (any library; PMC passes)")
     a = ap.parse_args()
     cfg = config.default_config()
     eng = NativeCodec(cfg, weights.synthetic_state_dict(cfg, seed=1), "cuda:0", gemm="x6")
     eng.set_knob("DCX_H3", 1)
-    f = _native.lib().dcx_diag_seg
-    f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-    for st in [int(s) for s in a.stages.split(",")]:
-        C = cfg["decoder"]["upsample_initial_channel"] >> (st + 1)
+    f = None
+    if not a.no_diag:
+        f = _native.lib().dcx_diag_seg
+        f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    jobs = []
+    if a.blocks:
+        for blk in a.blocks.split(","):
+            C = cfg["encoder"]["dims"][int(blk.split(".")[0])]
+            jobs.append((f"encoder.stages.{blk}", C))
+    else:
+        for st in [int(s) for s in a.stages.split(",")]:
+            jobs.append((f"generator.resblocks.{st}", cfg["decoder"]["upsample_initial_channel"] >> (st + 1)))
+    for mod, C in jobs:
         x = torch.randn(4, a.rows // 4, C, device="cuda")
-        eng.module(f"generator.resblocks.{st}", x)
+        eng.module(mod, x)
         torch.cuda.synchronize()
+        if f is None:
+            for _ in range(3):
+                eng.module(mod, x)
+            torch.cuda.synchronize()
+            print(f"{mod} (C = {C}) done", flush=True)
+            continue
         out = (ctypes.c_ulonglong * 13)()
         f(out, 1)
         for _ in range(3):
-            eng.module(f"generator.resblocks.{st}", x)
+            eng.module(mod, x)
         torch.cuda.synchronize()
         f(out, 1)
         n = max(out[12], 1)
         v = [out[i] / n for i in range(12)]
         lab = ["mfma", "wait", "mem", "wait", "(dma issue", "reads"]
         for g in range(2):
-            print(f"stage {st} (C = {C}) g{g}: " + "  ".join(f"{lab[i]} {v[6 * g + i]:6.0f}" for i in range(6))
+            print(f"{mod} (C = {C}) g{g}: " + "  ".join(f"{lab[i]} {v[6 * g + i]:6.0f}" for i in range(6))
                   + f")  | step {sum(v[6 * g:6 * g + 4]):6.0f}", flush=True)
 
 
