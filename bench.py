@@ -420,9 +420,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "arith": ("fp32 operands split into 3 bf16 planes, 6 exact bf16 products per fp32 product, fp32 "
-                      "accumulation (v_mfma_f32_16x16x32_bf16 / 32x32x16_bf16)" if args.gemm == "x6" else
-                      "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
+            "arith": ("fp32-accurate: the wide generator convs and the ConvNeXt 1x1 convs as 2 fp16 values per "
+                      "operand (h, l), 3 exact fp16 products per fp32 product (v_mfma_f32_16x16x32_f16, 'h3'); the "
+                      "rest as 3 bf16 planes, 6 exact bf16 products (v_mfma_f32_16x16x32_bf16 / 32x32x16_bf16, 'x6'); "
+                      "fp32 accumulation" if args.gemm == "x6" else "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
             "data": "synthetic (speech/music-like 24 kHz clips; seeded synthetic weights, no checkpoint offline)",
             "config": {"workload": workload, "global_batch": n_total, "clip_samples_max": longest,
                        "frames_per_clip": frames, "parallelism": f"clip-sharded x{world}, codes all_gather",

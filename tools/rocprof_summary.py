@@ -37,6 +37,19 @@ def short(name):
         return f"{base}<{65536 // int(parts[0])},{parts[0]},halo>"
     if base == "conv_gemm_x6dq":  # <BN>, halo
         return f"{base}<{65536 // int(parts[0])},{parts[0]},halo>"
+    if base == "conv_gemm_x3dw_group":
+        return "conv_gemm_x3dw_group<256,256,halo>"
+    if base == "conv_gemm_x3dw":  # <HALO>
+        return "conv_gemm_x3dw<256,256,halo>" if parts and parts[0] != "0" else "conv_gemm_x3dw<256,256>"
+    if base == "conv_gemm_x3dq_group":  # <BN>, halo
+        return f"{base}<{32768 // int(parts[0])},{parts[0]},halo>"
+    if base == "conv_gemm_x3dq":  # <BN, HALO>; HALO = 0: the one-tap conv_gemm_x3dm
+        bm, bn = 32768 // int(parts[0]), int(parts[0])
+        return f"conv_gemm_x3dq<{bm},{bn},halo>" if parts[1] != "0" else f"conv_gemm_x3dm<{bm},{bn}>"
+    if base == "vq_prefilter_b1":
+        return "vq_prefilter_b1<256,256>"
+    if base in ("conv_res_pair", "conv_res_pair_g", "conv_res_pair_w4"):  # <C, MEAN, ROWS>
+        return f"{base}<{parts[0]}{',mean' if len(parts) > 1 and parts[1] == 'true' else ''}>"
     if base == "vq_prefilter_dm":  # <XMID>
         return "vq_prefilter_dm<256,256>" if parts and parts[0] == "true" else "vq_prefilter_dm_x2<256,256>"
     if base == "vq_prefilter_x3":
