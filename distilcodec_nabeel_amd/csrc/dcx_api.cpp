@@ -645,6 +645,7 @@ int* knob_slot(dcx::Knobs& k, const std::string& n) {
   if (n == "DCX_H3") return &k.h3;
   if (n == "DCX_H3_BN") return &k.h3_bn;
   if (n == "DCX_H3_1X1") return &k.h3_1x1;
+  if (n == "DCX_H3_SPLIT") return &k.h3_split;
   return nullptr;
 }
 
@@ -652,7 +653,8 @@ void knobs_from_env(dcx::Knobs& k) {
   static const char* const names[] = {"DCX_RP_R",         "DCX_RP_OLD",       "DCX_RP_G64",       "DCX_RP_SYNC",
                                       "DCX_RP_W4",        "DCX_GELU_LUT",     "DCX_BF16_PERSIST", "DCX_BF16_REG_EPI",
                                       "DCX_DWCONV_TILED", "DCX_SPLIT_MIN_STEPS", "DCX_SPLIT_GROUP_OFF",
-                                      "DCX_H3",           "DCX_H3_BN",        "DCX_H3_1X1"};
+                                      "DCX_H3",           "DCX_H3_BN",        "DCX_H3_1X1",
+                                      "DCX_H3_SPLIT"};
   for (const char* n : names) {
     const char* e = std::getenv(n);
     if (e && *e) *knob_slot(k, n) = std::atoi(e);

@@ -2587,19 +2587,26 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x3dq_group(const ConvGroup g
 //     c - 2's last step, MEM1((c - 1) * taps - 1)) is at least two segments earlier for taps >= 2.
 // Per-lane DMA offsets are one VGPR per operand (row base) plus a wave-uniform add per piece.
 // ---------------------------------------------------------------------------------------------
-template <int HALO>
+// SPLIT (Knobs::h3_split): the weight pieces of step s + 2 are issued half by group 0 in MEM0(s)
+// and half by group 1 in MEM1(s) (one tap: group 0 the input pieces, group 1 all weight pieces), so
+// the CU fetches during both segments.  Group 1 may overwrite step s's slot only once all four of its
+// waves have read their step-s fragments: each wave, once its reads have returned, bumps an LDS
+// counter, and waits for it to reach 4 (s + 1) before issuing.  Group 1 retires its pieces at the
+// end of MEM1(s + 1), before the barrier that opens MEM0(s + 1), their first reader.
+template <int HALO, bool SPLIT>
 __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, const int b, const int ph) {
   constexpr int BM = 256, BN = 256, WN = 2, WM = 4;
   constexpr int WR = 64, WC = 128, TM = 4, TN = 8;
   constexpr int AR = BM + HALO;                 // rows of an input image
   constexpr int A_N = AR / 8, B_N = BN / 8;     // 1 KiB DMA instructions per A chunk / B step
-  constexpr int A_PW = A_N / 4, B_PW = B_N / 4; // per group-0 wave
+  constexpr int A_PW = A_N / 4;                 // A pieces per group-0 wave
   constexpr int ABUF = AR * 128, BBUF = BN * 128;  // bytes
   constexpr int NA = 2;                         // A buffers (halo: chunk parity; one tap: step slot)
   constexpr int LDS_B = NA * ABUF + 2 * BBUF;
   static_assert(A_N % 4 == 0 && B_N % 4 == 0 && AR % 64 == 0, "tile shape");
-  static_assert(LDS_B <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) unsigned short lds[LDS_B / 2];
+  static_assert(LDS_B + 16 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned short lds[LDS_B / 2 + 8];  // + group 1's read counter
+  unsigned int* const rd_cnt = reinterpret_cast<unsigned int*>(lds + LDS_B / 2);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int group = __builtin_amdgcn_readfirstlane(tid >> 8);
@@ -2639,22 +2646,32 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
     const int abuf = HALO ? (c & 1) : slot;
     dma16(rx, lds + abuf * (ABUF / 2) + k * 512, a_lane + row * arow + (pc & 3) * 32 + (pc >> 2) * 16 + c * 128, 0);
   };
+  // B instructions [0, B_G0) are group 0's, [B_G0, B_N) group 1's (SPLIT)
+#ifndef DCX_X3W_BG0_DIV  // A/B builds: group 0's share of the weight pieces, 1 / DIV (halo convs)
+#define DCX_X3W_BG0_DIV 2
+#endif
+  constexpr int B_G0 = !SPLIT ? B_N : HALO ? B_N / DCX_X3W_BG0_DIV : 0;
+  constexpr int B_W0 = B_G0 / 4, B_W1 = (B_N - B_G0) / 4;  // B pieces per wave of group 0 / 1
   auto dmaB1 = [&](int c, int m, int slot, int i) {  // the wave's i-th B piece of step (c, m)
 #ifdef DCX_X3_NODMA
     if (in_loop) return;
 #endif
-    const int k = i * 4 + gw;
+    const int k = (group ? B_G0 : 0) + i * 4 + gw;
     const int u = k * 64, pc = u / BN, col = u - pc * BN;
     dma16(rw, lds + NA * ABUF / 2 + slot * (BBUF / 2) + k * 512, b_lane + col * 128 + (pc & 3) * 32 + (pc >> 2) * 16,
           (m * nchunks + c) * p.Cout * 128);
   };
-  auto dma_step = [&](int c, int m, int slot) {  // a step's pieces (its input chunk first when it opens one)
+  auto dma_step = [&](int c, int m, int slot) {  // group 0's pieces of a step (its input chunk first)
     if (m == 0) {
 #pragma unroll
       for (int i = 0; i < A_PW; ++i) dmaA1(c, slot, i);
     }
 #pragma unroll
-    for (int i = 0; i < B_PW; ++i) dmaB1(c, m, slot, i);
+    for (int i = 0; i < B_W0; ++i) dmaB1(c, m, slot, i);
+  };
+  auto dma_step1 = [&](int c, int m, int slot) {  // group 1's (SPLIT)
+#pragma unroll
+    for (int i = 0; i < B_W1; ++i) dmaB1(c, m, slot, i);
   };
 
   // fragment addresses: one lane base per operand (h piece of the lane's channel group kg); the
@@ -2702,10 +2719,12 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
     if (++m_ == taps) { m_ = 0; ++c_; }
   };
 
-  // prologue: steps 0 and 1 (group 0 issues), drained
-  int cl = 0, ml = 0;  // the next step group 0 issues
+  // prologue: steps 0 and 1, drained
+  int cl = 0, ml = 0;  // the next step this group issues
+  if (SPLIT && tid == 0) *rd_cnt = 0u;
   for (int t = 0; t < 2 && t < nsteps; ++t) {
     if (group == 0) dma_step(cl, ml, t);
+    else if (SPLIT) dma_step1(cl, ml, t);
     adv(cl, ml);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2745,6 +2764,20 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
     for (int s = 0; s < nsteps; ++s) {
       DCX_SEGT(ta);
       readF(cr, mr, s & 1);  // MEM1(s): fragments of step s
+      if (SPLIT) {
+        int n = 0;
+        if (s + 2 < nsteps) {  // this group's pieces of step s + 2, into step s's slot once read
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (lane == 0) __hip_atomic_fetch_add(rd_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const unsigned int want = 4u * (unsigned)(s + 1);
+          while (__hip_atomic_load(rd_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
+          }
+          dma_step1(cl, ml, s & 1);
+          adv(cl, ml);
+          n = B_W1;
+        }
+        wait_dma(n);  // step s + 1's pieces (issued in MEM1(s - 1)) landed
+      }
       DCX_SEGT(tb);
       seg_barrier();
       DCX_SEGT(tc);
@@ -2774,13 +2807,14 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
   epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
-template <int HALO>
+template <int HALO, bool SPLIT>
 __global__ void __launch_bounds__(512, 2) conv_gemm_x3dw(const ConvParams p) {
   int wg, b, ph;
   flat_tile(((p.Lq + 255) / 256) * (p.Cout / 256), p.batch, wg, b, ph);
-  x3dw_tile<HALO>(p, wg, b, ph);
+  x3dw_tile<HALO, SPLIT>(p, wg, b, ph);
 }
 
+template <bool SPLIT>
 __global__ void __launch_bounds__(512, 2) conv_gemm_x3dw_group(const ConvGroup g) {
   const int t = blockIdx.x;
   const int k = t >= g.start[1] ? (t >= g.start[2] ? 2 : 1) : 0;
@@ -2790,7 +2824,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x3dw_group(const ConvGroup g
   if (k == 0) p = g.p[0];
   else if (k == 1) p = g.p[1];
   else p = g.p[2];
-  x3dw_tile<64>(p, local - b * g.tiles_per_clip[k], b, 0);
+  x3dw_tile<64, SPLIT>(p, local - b * g.tiles_per_clip[k], b, 0);
 }
 
 // Whether conv_gemm_x3dq<bn> (taps >= 3 with a halo) or conv_gemm_x3dm<bn> (one tap) takes an h3
@@ -4365,12 +4399,15 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
       ConvParams q = p;
       q.batch = batch;
       q.phases = phases;
+      const bool sp = knobs(p).h3_split;
       if (p.taps == 1) {
         if (kname) *kname = "conv_gemm_x3dw<256,256>";
-        hipLaunchKernelGGL((conv_gemm_x3dw<0>), grid, dim3(512), 0, s, q);
+        if (sp) hipLaunchKernelGGL((conv_gemm_x3dw<0, true>), grid, dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((conv_gemm_x3dw<0, false>), grid, dim3(512), 0, s, q);
       } else {
         if (kname) *kname = "conv_gemm_x3dw<256,256,halo>";
-        hipLaunchKernelGGL((conv_gemm_x3dw<64>), grid, dim3(512), 0, s, q);
+        if (sp) hipLaunchKernelGGL((conv_gemm_x3dw<64, true>), grid, dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((conv_gemm_x3dw<64, false>), grid, dim3(512), 0, s, q);
       }
       return hipGetLastError();
     }
@@ -4522,7 +4559,8 @@ hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t
     for (int k = n; k <= kMaxGroup; ++k) g.start[k] = (int)start;
     if (bsel == 512) {
       if (kname) *kname = "conv_gemm_x3dw_group<256,256,halo>";
-      hipLaunchKernelGGL(conv_gemm_x3dw_group, dim3((unsigned)start), dim3(512), 0, s, g);
+      if (knobs(ps[0]).h3_split) hipLaunchKernelGGL(conv_gemm_x3dw_group<true>, dim3((unsigned)start), dim3(512), 0, s, g);
+      else hipLaunchKernelGGL(conv_gemm_x3dw_group<false>, dim3((unsigned)start), dim3(512), 0, s, g);
     } else if (bn == 256) {
       if (kname) *kname = "conv_gemm_x3dq_group<128,256,halo>";
       hipLaunchKernelGGL((conv_gemm_x3dq_group<256>), dim3((unsigned)start), dim3(512), 0, s, g);

@@ -38,6 +38,7 @@ struct Knobs {
   int split_group_off = 0;  // DCX_SPLIT_GROUP_OFF=1: per-conv split launches instead of grouped ones
   int h3 = 1;               // DCX_H3=0: the wide generator stages' ResBlock convs in x6 arithmetic (A/B, tests)
   int h3_bn = 0;            // DCX_H3_BN=128 / 256: the 256 x 128 / 128 x 256 h3 tiles instead of 256 x 256 (A/B)
+  int h3_split = 1;         // DCX_H3_SPLIT=0: conv_gemm_x3dw's DMA issued by group 0 alone (A/B)
   int h3_1x1 = 1;           // DCX_H3_1X1=0: the ConvNeXt blocks' 1x1 convs in x6 arithmetic (A/B, tests)
 };
 
