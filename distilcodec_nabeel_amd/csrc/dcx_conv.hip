@@ -230,6 +230,16 @@ extern "C" int dcx_diag_seg(unsigned long long* out13, int reset) {
   }
   return 0;
 }
+// conv_gemm_x3dw: the same six sums for every wave of the workgroup, [wave * 6 + i], [48] steps
+__device__ unsigned long long g_seg_diag8[49];
+extern "C" int dcx_diag_seg8(unsigned long long* out49, int reset) {
+  if (hipMemcpyFromSymbol(out49, HIP_SYMBOL(g_seg_diag8), sizeof(unsigned long long) * 49) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned long long z[49] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_seg_diag8), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
 #define DCX_SEGT(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #else
 #define DCX_SEGT(v)
@@ -2745,6 +2755,15 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
       seg_barrier();
       DCX_SEGT(tc);
       // MEM0(s): issue step s + 2 into step s's slot, fragments of step s + 1
+#ifdef DCX_X3W_READFIRST
+      if (s + 1 < nsteps) readF(cr, mr, (s + 1) & 1);
+      DCX_SEGT(tr);
+      if (s + 2 < nsteps) {
+        dma_step(cl, ml, s & 1);
+        adv(cl, ml);
+      }
+      DCX_SEGT(tq);
+#else
       if (s + 2 < nsteps) {
         dma_step(cl, ml, s & 1);
         adv(cl, ml);
@@ -2752,6 +2771,7 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
       DCX_SEGT(tr);
       if (s + 1 < nsteps) readF(cr, mr, (s + 1) & 1);
       DCX_SEGT(tq);
+#endif
       DCX_SEGT(td);
       seg_barrier();
       DCX_SEGT(te);
@@ -2796,6 +2816,11 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
 #pragma unroll
     for (int i = 0; i < 6; ++i) atomicAdd(&g_seg_diag[group * 6 + i], sd[i]);
     if (group == 0) atomicAdd(&g_seg_diag[12], (unsigned long long)nsteps);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) atomicAdd(&g_seg_diag8[wave * 6 + i], sd[i]);
+    if (wave == 0) atomicAdd(&g_seg_diag8[48], (unsigned long long)nsteps);
   }
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--rows", type=int, default=19200, help="rows (B * L) of the stage input")
     ap.add_argument("--blocks", default="", help="encoder ConvNeXt blocks instead (conv_gemm_x3dm), e.g. 0.0,2.0")
     ap.add_argument("--no-diag", action="store_true", help="run the modules only (any library; PMC passes)")
+    ap.add_argument("--per-wave", action="store_true", help="conv_gemm_x3dw: every wave's sums (dcx_diag_seg8)")
     a = ap.parse_args()
     cfg = config.default_config()
     eng = NativeCodec(cfg, weights.synthetic_state_dict(cfg, seed=1), "cuda:0", gemm="x6")
@@ -59,6 +60,19 @@ def main():
             eng.module(mod, x)
         torch.cuda.synchronize()
         f(out, 1)
+        if a.per_wave:
+            g8 = _native.lib().dcx_diag_seg8
+            g8.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+            o8 = (ctypes.c_ulonglong * 49)()
+            g8(o8, 1)
+            for _ in range(3):
+                eng.module(mod, x)
+            torch.cuda.synchronize()
+            g8(o8, 1)
+            n8 = max(o8[48], 1)
+            for w in range(8):
+                v = [o8[w * 6 + i] / n8 for i in range(6)]
+                print(f"{mod} wave {w}: " + "  ".join(f"{v[i]:6.0f}" for i in range(6)), flush=True)
         n = max(out[12], 1)
         v = [out[i] / n for i in range(12)]
         lab = ["mfma", "wait", "mem", "wait", "(dma issue", "reads"]
