@@ -2754,16 +2754,8 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
       DCX_SEGT(tb);
       seg_barrier();
       DCX_SEGT(tc);
-      // MEM0(s): issue step s + 2 into step s's slot, fragments of step s + 1
-#ifdef DCX_X3W_READFIRST
-      if (s + 1 < nsteps) readF(cr, mr, (s + 1) & 1);
-      DCX_SEGT(tr);
-      if (s + 2 < nsteps) {
-        dma_step(cl, ml, s & 1);
-        adv(cl, ml);
-      }
-      DCX_SEGT(tq);
-#else
+      // MEM0(s): issue step s + 2 into step s's slot, fragments of step s + 1 (reads first: same
+      // times, r05q)
       if (s + 2 < nsteps) {
         dma_step(cl, ml, s & 1);
         adv(cl, ml);
@@ -2771,7 +2763,6 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
       DCX_SEGT(tr);
       if (s + 1 < nsteps) readF(cr, mr, (s + 1) & 1);
       DCX_SEGT(tq);
-#endif
       DCX_SEGT(td);
       seg_barrier();
       DCX_SEGT(te);
