@@ -365,9 +365,9 @@ struct Builder {
           }
     return upload16(out);
   }
-  // fp32 packed [cout][taps][cin] (one phase) -> h3 layout [tap][cin/32][cout][4 groups][h 8 | l 8]
-  // fp16 of w * 2^shift, shift putting the largest |w| in [2^14, 2^15) (conv_gemm_x3dq)
-  unsigned short* h2_pack(const std::vector<float>& pk, int cout, int taps, int cin, int& shift) {
+  // fp32 packed [phases][cout][taps][cin] -> h3 layout [phase][tap][cin/32][cout][4 groups][h 8 | l 8]
+  // fp16 of w * 2^shift, shift putting the largest |w| in [2^14, 2^15) (conv_gemm_x3dq / x3dw)
+  unsigned short* h2_pack(const std::vector<float>& pk, int phases, int cout, int taps, int cin, int& shift) {
     if (bad() || dry) return nullptr;
     float mx = 0.f;
     for (float v : pk) mx = std::max(mx, std::fabs(v));
@@ -375,12 +375,13 @@ struct Builder {
     if (mx > 0.f) std::frexp(mx, &e);  // mx = f * 2^e, f in [0.5, 1)
     shift = mx > 0.f ? 15 - e : 0;
     const int nch = cin / 32;
-    std::vector<unsigned short> out((size_t)taps * nch * cout * 64);
+    std::vector<unsigned short> out((size_t)phases * taps * nch * cout * 64);
+    for (int r = 0; r < phases; ++r)
     for (int m = 0; m < taps; ++m)
       for (int c = 0; c < nch; ++c)
         for (int o = 0; o < cout; ++o) {
-          unsigned short* dst = &out[(((size_t)m * nch + c) * cout + o) * 64];
-          const float* src = &pk[((size_t)o * taps + m) * cin + c * 32];
+          unsigned short* dst = &out[((((size_t)r * taps + m) * nch + c) * cout + o) * 64];
+          const float* src = &pk[(((size_t)r * cout + o) * taps + m) * cin + c * 32];
           for (int j = 0; j < 32; ++j) {
             const float x = std::ldexp(src[j], shift);
             const _Float16 hh = (_Float16)x;
@@ -463,7 +464,7 @@ struct Builder {
     c.w = upload(pk);
     if (cin % 16 == 0) c.w6 = split_pack(pk, 1, cout, k, cin);
     if (k == 1 && cin % 32 == 0) c.wc = compact_pack(pk, cout, cin);
-    if (h3 && cin % 32 == 0) c.w3 = h2_pack(pk, cout, k, cin, c.w3_shift);
+    if (h3 && cin % 32 == 0) c.w3 = h2_pack(pk, 1, cout, k, cin, c.w3_shift);
     if (has_bias) {
       c.b = vec(prefix + ".bias", cout);
       c.b16 = vec_bf16(prefix + ".bias", cout);
@@ -473,7 +474,7 @@ struct Builder {
 
   // ConvTranspose1d weight [Cin][Cout][k], stride s, padding (k-s)/2 -> s polyphase convs:
   // output o = q*s + r reads input q + base_r - m with tap j = (r+p)%s + m*s, m < k/s.
-  ConvW convT(const std::string& prefix, int cin, int cout, int k, int s) {
+  ConvW convT(const std::string& prefix, int cin, int cout, int k, int s, bool h3 = false) {
     ConvW c;
     const int p = (k - s) / 2, taps = k / s;
     c.cin = cin; c.cout = cout; c.taps = taps; c.phases = s; c.in_step = -1; c.out_mul = s;
@@ -490,6 +491,7 @@ struct Builder {
     }
     c.w = upload(pk);
     if (cin % 16 == 0) c.w6 = split_pack(pk, s, cout, taps, cin);
+    if (h3 && cin % 32 == 0) c.w3 = h2_pack(pk, s, cout, taps, cin, c.w3_shift);
     c.b = vec(prefix + ".bias", cout);
     c.b16 = vec_bf16(prefix + ".bias", cout);
     return c;
@@ -723,6 +725,12 @@ int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32,
 bool takes_compact(const dcx_codec* h, const ConvW& w, long long rows) {
   return h->compact && h->gemm_mode == DCX_GEMM_BF16 && w.wc && w.taps == 1 && w.phases == 1 && w.in_base[0] == 0 &&
          rows < (1LL << 31) && dcx::bf16dm_takes(w.cin, w.cout, (int)rows, w.cin, 1);
+}
+
+// Whether a generator conv with a tap halo (conv_pre, the wide ConvTs) runs in h3 arithmetic
+// (conv_gemm_x3dw; Knobs::h3, x6 mode, not in the split-K latency mode), so its producer writes h2.
+bool takes_h3_conv(const dcx_codec* h, const ConvW& w) {
+  return h->knobs.h3 && h->gemm_mode == DCX_GEMM_X6 && h->split_k < 2 && w.w3 && w.taps >= 2 && w.cout % 256 == 0;
 }
 
 // Whether a one-tap conv runs in h3 arithmetic (conv_gemm_x3dm; Knobs::h3_1x1, x6 mode, not in the
@@ -979,15 +987,19 @@ ConvCall framed(CAct x, int B, int L, int C) {
   } while (0)
 
 // fp32 -> planes (or, with compact, bf16) for a tensor handed in by the caller (x6 / bf16 modes).
-int ensure_planes(dcx_codec* h, CAct& a, long long rows, int C, Bump& ws, hipStream_t s, bool compact = false) {
+// h2: the h2 layout instead (an h3 consumer; a planes tensor handed in with its fp32 copy is re-split)
+int ensure_planes(dcx_codec* h, CAct& a, long long rows, int C, Bump& ws, hipStream_t s, bool compact = false,
+                  bool h2 = false) {
+  if (h2 && a.p && !a.h2 && a.f) a.p = nullptr;
   if (!x6_mode(h) || a.p) return DCX_OK;
   unsigned short* p = ws.u16((size_t)rows * C * 3);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small");
-  LAUNCH(h, s, "split_planes", 0, (compact ? 6.0 : 10.0) * rows * C,
-         dcx::launch_split_planes(a.f, p, rows, C, compact ? 1 : 0, s));
+  LAUNCH(h, s, "split_planes", 0, (compact ? 6.0 : h2 ? 8.0 : 10.0) * rows * C,
+         dcx::launch_split_planes(a.f, p, rows, C, compact ? 1 : h2 ? 3 : 0, s));
   a.p = p;
   a.c1 = compact;
+  a.h2 = h2 && !compact;
   return DCX_OK;
 }
 
@@ -995,7 +1007,7 @@ int ensure_planes(dcx_codec* h, CAct& a, long long rows, int C, Bump& ws, hipStr
 // with out6c) of the block output for a following conv.  ln: [M][C], hid: [M][4C] conv-input
 // scratch, written compact where their consumer takes it (bf16 mode).
 int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, int B, int T, Act ln, Act hid,
-              hipStream_t s, bool out6c = false) {
+              hipStream_t s, int out6c = 0) {
   const long long M = (long long)B * T;
   const int C = bw.C;
   ln.c1 = ln.p && takes_compact(h, bw.pw1, M);
@@ -1012,7 +1024,7 @@ int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, in
   ConvCall c2 = pointwise(hid, M);
   c2.y = x;
   c2.y6 = out6;
-  c2.y6c = out6 && out6c ? 1 : 0;
+  c2.y6c = out6 ? out6c : 0;  // 0 planes, 1 compact, 3 h2
   c2.res = x;
   c2.gamma = bw.gamma;
   c2.epi = dcx::EPI_GAMMA_RES;
@@ -1257,7 +1269,7 @@ int stage_vq_decode(dcx_codec* h, const int32_t* codes, int B, int T, Act z, int
   ConvCall cu = pointwise(zd, M);
   cu.y = z.f;
   RUN(run_conv(h, h->vq_up, cu, s));
-  RUN(run_block(h, h->vq_up_blk, z.f, z.p, B, T, ln, hid, s));
+  RUN(run_block(h, h->vq_up_blk, z.f, z.p, B, T, ln, hid, s, z.h2 ? 3 : 0));
   return DCX_OK;
 }
 
@@ -1417,7 +1429,7 @@ int run_parallel_block(dcx_codec* h, int i, int B, int Lo, const PBlockBufs& b, 
 
 int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hipStream_t s) {
   const dcx_config& c = h->cfg;
-  RUN(ensure_planes(h, z, (long long)B * T, c.vq_dim, ws, s));
+  RUN(ensure_planes(h, z, (long long)B * T, c.vq_dim, ws, s, false, takes_h3_conv(h, h->conv_pre)));
   const size_t per = (size_t)B * T * max_gen_width(c);
   // The ParallelBlock's ResBlocks are independent until the mean, so each keeps its own state and
   // the convs of one dilation index run as one grouped launch (run_conv_group).
@@ -1445,14 +1457,17 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
   int C = c.gen_channels, L = T;
   {  // conv_pre, then the first stage's SiLU (generators.py:121,125) fused as the only output
     ConvCall cc = framed(z, B, T, c.vq_dim);
-    cc.silu_to(S);
+    Act S0 = S;
+    S0.h2 = S.p && takes_h3_conv(h, h->ups[0]);
+    cc.silu_to(S0);
     RUN(run_conv(h, h->conv_pre, cc, s));
   }
   for (int i = 0; i < c.n_ups; ++i) {
     const ConvW& up = h->ups[i];
     const int Co = up.cout, Lo = L * c.up_rates[i];
     const ConvW& rconv = h->res[i][0][0][0];  // every ResBlock conv of the stage has Cin = Cout = Co
-    const Act S_i = in_form(S, up);
+    Act S_i = in_form(S, up);
+    S_i.h2 = S_i.p && takes_h3_conv(h, up);  // as conv_pre / the previous stage's mean epilogue wrote it
     Act XS_i = in_form(XS, rconv);
     Act RS_i[NR], Tb_i[NR];
     for (int rb = 0; rb < c.n_res; ++rb) {
@@ -1483,7 +1498,10 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
     }
     pb.Mx = Mx;
     pb.last = i == c.n_ups - 1;
-    if (!pb.last) pb.next = in_form(S, h->ups[i + 1]);
+    if (!pb.last) {
+      pb.next = in_form(S, h->ups[i + 1]);
+      pb.next.h2 = pb.next.p && takes_h3_conv(h, h->ups[i + 1]);
+    }
     RUN(run_parallel_block(h, i, B, Lo, pb, s));
     C = Co;
     L = Lo;
@@ -1506,6 +1524,7 @@ int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int3
   Act z;
   z.f = ws.f((size_t)M * c.vq_dim);
   if (x6_mode(h)) z.p = ws.u16((size_t)M * c.vq_dim * 3);
+  z.h2 = z.p && h->has_gen && takes_h3_conv(h, h->conv_pre);  // conv_pre's input as the VQ up block writes it
   const size_t mark = ws.off;
   size_t need = mark;
   auto sub = [&](auto fn) -> int {  // each sub-stage reuses the tail of the workspace
@@ -1675,7 +1694,7 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
   if (!h->has_gen && m.rfind("generator.", 0) == 0) return fail(h, DCX_ERR_STATE, "generator weights were not finalized");
   if (m == "generator.conv_pre") {  // generators.py:121
     CAct in(x, nullptr);
-    RUN(ensure_planes(h, in, M, c.vq_dim, ws, s));
+    RUN(ensure_planes(h, in, M, c.vq_dim, ws, s, false, takes_h3_conv(h, h->conv_pre)));
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
     ConvCall cc = framed(in, B, L, c.vq_dim);
@@ -1699,7 +1718,7 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
   if (match_idx(m, "generator.ups.%d%n", &a) && a >= 0 && a < c.n_ups) {
     const ConvW& up = h->ups[a];
     CAct in(x, nullptr);
-    if (!(x6_mode(h) && f32_input_ok(up))) RUN(ensure_planes(h, in, M, up.cin, ws, s));
+    if (!(x6_mode(h) && f32_input_ok(up))) RUN(ensure_planes(h, in, M, up.cin, ws, s, false, takes_h3_conv(h, up)));
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
     ConvCall cc = framed(in, B, L, up.cin);
@@ -2033,9 +2052,12 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
   if (with_generator) {
     const std::string g = "generator.";
     int ch = c.gen_channels;
-    h->conv_pre = B.conv(g + "conv_pre", c.vq_dim, ch, c.gen_pre_k, 1, (c.gen_pre_k - 1) / 2);
+    // h3 weights for the convs conv_gemm_x3dw takes (Cout % 256 == 0, two taps or more)
+    h->conv_pre = B.conv(g + "conv_pre", c.vq_dim, ch, c.gen_pre_k, 1, (c.gen_pre_k - 1) / 2, true,
+                         ch % 256 == 0 && c.gen_pre_k >= 2);
     for (int i = 0; i < c.n_ups; ++i) {
-      h->ups[i] = B.convT(g + "ups." + std::to_string(i), ch, ch / 2, c.up_kernels[i], c.up_rates[i]);
+      h->ups[i] = B.convT(g + "ups." + std::to_string(i), ch, ch / 2, c.up_kernels[i], c.up_rates[i],
+                          (ch / 2) % 256 == 0 && c.up_kernels[i] / c.up_rates[i] >= 2);
       ch /= 2;
       for (int rb = 0; rb < c.n_res; ++rb) {
         const int k = c.res_kernels[rb];

@@ -2845,7 +2845,8 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x3dw_group(const ConvGroup g
 
 // Whether conv_gemm_x3dq<bn> (taps >= 3 with a halo) or conv_gemm_x3dm<bn> (one tap) takes an h3
 // conv (input in the h2 layout, x_compact == 3).
-static bool x3dq_ok(const ConvParams& p, int bn) {
+// wide (conv_gemm_x3dw): taps >= 2 (its input buffer is free two segments before it is refilled)
+static bool x3dq_ok(const ConvParams& p, int bn, bool wide = false) {
   const int span = (p.taps - 1) * (p.in_step < 0 ? -p.in_step : p.in_step);
   if (!p.x6 || !p.w3 || p.x_compact != 3 || p.Cin % 32 || p.Cout % bn || p.ksplit > 1) return false;
   const long long arow = (long long)p.ldx * 4;
@@ -2855,7 +2856,7 @@ static bool x3dq_ok(const ConvParams& p, int bn) {
       if (p.in_base[i] < 0) return false;
     return 256LL * arow < (1LL << 31);
   }
-  return p.taps >= 3 && span > 0 && span <= 64 && (long long)(p.Lin + 1024) * arow < (1LL << 31);
+  return p.taps >= (wide ? 2 : 3) && span > 0 && span <= 64 && (long long)(p.Lin + 1024) * arow < (1LL << 31);
 }
 // Tiles of an h3 conv: 256 x 256 (conv_gemm_x3dw) where Cout % 256 == 0, else 256 x 128.  (256 x 128
 // against 128 x 256: half the weight DMA per step, C2 205.1 -> 193.2 ms, r05i.)  Knobs::h3_bn
@@ -4409,7 +4410,7 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
   if (p.Cin % BK || p.Cout % 32 || phases < 1 || phases > kMaxPhases) return hipErrorInvalidValue;
   if (p.x_compact == 3) {  // h2 input: the h3 kernels only
     const int bn = x3dq_bn(p);
-    if (!x3dq_ok(p, bn == 512 ? 256 : bn)) return hipErrorInvalidValue;
+    if (!x3dq_ok(p, bn == 512 ? 256 : bn, bn == 512)) return hipErrorInvalidValue;
     if (bn == 512) {
       const dim3 grid((unsigned)(((p.Lq + 255) / 256) * (p.Cout / 256) * batch * phases));
       ConvParams q = p;

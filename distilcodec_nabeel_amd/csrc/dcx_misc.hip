@@ -409,12 +409,13 @@ __global__ void __launch_bounds__(256) split_planes_kernel(const float* __restri
     const long long i = i4 * 4;
     if (compact == 1) store_bf16x4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
     else if (compact == 2) store_hm4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
+    else if (compact == 3) store_h2_4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
     else store_planes4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
   }
 }
 
 hipError_t launch_split_planes(const float* x, unsigned short* y6, long long rows, int C, int compact, hipStream_t s) {
-  if (C % 8 || compact < 0 || compact > 2 || (compact == 2 && C % 32)) return hipErrorInvalidValue;
+  if (C % 8 || compact < 0 || compact > 3 || (compact >= 2 && C % 32)) return hipErrorInvalidValue;
   const long long total4 = rows * C / 4;
   unsigned g = (unsigned)((total4 + 255) / 256);
   if (g > 8192) g = 8192;

@@ -133,3 +133,36 @@ def test_convnext_block_h3_vs_oracle(eng, golden, state):
     y3 = eng.module("encoder.stages.0.0", x).transpose(1, 2).cpu().numpy()
     assert _rel(y3, m["convnext256_out"]) < 2e-4
     assert not np.array_equal(y3, y6)  # the h3 path ran
+
+
+@pytest.mark.parametrize("i", [0, 1])
+def test_wide_conv_transpose_h3(eng, golden, i):
+    """ups[0] / ups[1] (Cout 512 / 256, 2 / 3 polyphase taps) on conv_gemm_x3dw against the
+    reference's fixture, as the x6 path."""
+    m = golden["modules"]
+    x = _cl(m[f"ups{i}_in"])
+    with eng.knobs(DCX_H3=0):
+        y6 = eng.module(f"generator.ups.{i}", x).transpose(1, 2).cpu().numpy()
+    y3 = eng.module(f"generator.ups.{i}", x).transpose(1, 2).cpu().numpy()
+    e6, e3 = _rel(y6, m[f"ups{i}_out"]), _rel(y3, m[f"ups{i}_out"])
+    assert e3 < 2e-4 and e3 < 4 * max(e6, 1e-7), (e3, e6)
+    assert not np.array_equal(y3, y6)  # the h3 path ran
+
+
+def test_conv_pre_h3(eng, state, cfg):
+    """conv_pre (k 13, 1024 -> 1024) on conv_gemm_x3dw against an fp64 conv1d of the same weights."""
+    from oracle import reference_cpu as R
+
+    d = cfg["decoder"]
+    sd = state["generator"]
+    x = torch.from_numpy(np.random.default_rng(7).standard_normal((2, cfg["quantizer"]["input_dim"], 300))
+                         .astype(np.float32))
+    k = d["pre_conv_kernel_size"]
+    ref = torch.nn.functional.conv1d(x.double(), R._w(sd, "conv_pre", torch.float64), R._t(sd, "conv_pre.bias", torch.float64),
+                                     padding=(k - 1) // 2).numpy()
+    with eng.knobs(DCX_H3=0):
+        y6 = eng.module("generator.conv_pre", _cl(x.numpy())).cpu().numpy().transpose(0, 2, 1)
+    y3 = eng.module("generator.conv_pre", _cl(x.numpy())).cpu().numpy().transpose(0, 2, 1)
+    e6, e3 = _rel(y6, ref), _rel(y3, ref)
+    print(f"\nconv_pre rel err: x6 {e6:.3g}, h3 {e3:.3g}")
+    assert e3 < 2e-5 and e3 < 4 * max(e6, 1e-7)
