@@ -648,6 +648,7 @@ int* knob_slot(dcx::Knobs& k, const std::string& n) {
   if (n == "DCX_H3_BN") return &k.h3_bn;
   if (n == "DCX_H3_1X1") return &k.h3_1x1;
   if (n == "DCX_H3_SPLIT") return &k.h3_split;
+  if (n == "DCX_H3_PAIRS") return &k.h3_pairs;
   return nullptr;
 }
 
@@ -656,7 +657,7 @@ void knobs_from_env(dcx::Knobs& k) {
                                       "DCX_RP_W4",        "DCX_GELU_LUT",     "DCX_BF16_PERSIST", "DCX_BF16_REG_EPI",
                                       "DCX_DWCONV_TILED", "DCX_SPLIT_MIN_STEPS", "DCX_SPLIT_GROUP_OFF",
                                       "DCX_H3",           "DCX_H3_BN",        "DCX_H3_1X1",
-                                      "DCX_H3_SPLIT"};
+                                      "DCX_H3_SPLIT",     "DCX_H3_PAIRS"};
   for (const char* n : names) {
     const char* e = std::getenv(n);
     if (e && *e) *knob_slot(k, n) = std::atoi(e);
@@ -1334,16 +1335,22 @@ int run_parallel_block(dcx_codec* h, int i, int B, int Lo, const PBlockBufs& b, 
       Rb[rb] = b.Tb[rb].f ? b.Tb[rb].f : reinterpret_cast<float*>(b.Tb[rb].p);
     }
     float* out = b.last ? b.Mx : b.next.f;
+    bool h3 = h->knobs.h3_pairs && h->split_k < 2;  // conv_res_pair_h3 (every conv with h3 weights)
+    for (int rb = 0; rb < c.n_res; ++rb)
+      for (int ci = 0; ci < 3; ++ci) h3 = h3 && h->res[i][rb][ci][0].w3 && h->res[i][rb][ci][1].w3;
     for (int ci = 0; ci < 3; ++ci) {
       dcx::ResPairParams rp{};
+      rp.h3 = h3 ? 1 : 0;
       double fl = 0, by = 0;
       for (int rb = 0; rb < c.n_res; ++rb) {
         const ConvW& w1 = h->res[i][rb][ci][0];
         const ConvW& w2 = h->res[i][rb][ci][1];
         rp.src[rb] = ci == 0 ? b.X : (ci == 1 ? Ra[rb] : Rb[rb]);
         rp.dst[rb] = ci == 0 ? Ra[rb] : (ci == 1 ? Rb[rb] : nullptr);
-        rp.w1[rb] = w1.w6;
-        rp.w2[rb] = w2.w6;
+        rp.w1[rb] = h3 ? w1.w3 : w1.w6;
+        rp.w2[rb] = h3 ? w2.w3 : w2.w6;
+        rp.w3_shift1[rb] = w1.w3_shift;
+        rp.w3_shift2[rb] = w2.w3_shift;
         rp.b1[rb] = w1.b;
         rp.b2[rb] = w2.b;
         rp.taps[rb] = w1.taps;
@@ -2064,7 +2071,7 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
         for (int j = 0; j < 3; ++j) {
           const int d = c.res_dilations[rb][j];
           const std::string p = g + "resblocks." + std::to_string(i) + ".blocks." + std::to_string(rb);
-          const bool h3 = ch % 128 == 0;  // the wide stages' convs (conv_gemm_x3dq tiles)
+          const bool h3 = ch % 32 == 0;  // conv_gemm_x3dq / x3dw tiles (C >= 128), conv_res_pair_h3 (32 / 64)
           h->res[i][rb][j][0] = B.conv(p + ".convs1." + std::to_string(j), ch, ch, k, d, (k * d - d) / 2, true, h3);
           h->res[i][rb][j][1] = B.conv(p + ".convs2." + std::to_string(j), ch, ch, k, 1, (k - 1) / 2, true, h3);
         }

@@ -39,6 +39,7 @@ struct Knobs {
   int h3 = 1;               // DCX_H3=0: the wide generator stages' ResBlock convs in x6 arithmetic (A/B, tests)
   int h3_bn = 0;            // DCX_H3_BN=128 / 256: the 256 x 128 / 128 x 256 h3 tiles instead of 256 x 256 (A/B)
   int h3_split = 1;         // DCX_H3_SPLIT=0: conv_gemm_x3dw's DMA issued by group 0 alone (A/B)
+  int h3_pairs = 1;         // DCX_H3_PAIRS=0: the C = 32 / 64 ResBlock pairs in x6 arithmetic (A/B, tests)
   int h3_1x1 = 1;           // DCX_H3_1X1=0: the ConvNeXt blocks' 1x1 convs in x6 arithmetic (A/B, tests)
 };
 
@@ -158,6 +159,9 @@ struct ResPairParams {
   // bounds how far the two waves of a SIMD drift apart before the image hand-offs (set by
   // launch_res_pair from kn)
   int tap_sync;
+  // h3 (conv_res_pair_h3): w1 / w2 are the ConvParams::w3 weights, scaled by 2^w3_shift{1,2}[m]
+  int h3;
+  int w3_shift1[kMaxGroup], w3_shift2[kMaxGroup];
   const Knobs* kn;  // host only; null = the defaults
 };
 

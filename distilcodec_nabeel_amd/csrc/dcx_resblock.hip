@@ -43,6 +43,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ float rp_silu(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
 // barrier that leaves global loads in flight (only LDS traffic is drained)
@@ -97,6 +98,27 @@ struct RpGeom {
   static constexpr int LDS = IMG + 2 * WSLOT + 2 * kMaxGroup * C * 4;
   static_assert(NB1 % WR == 0 && RB1 == RB2, "row blocks per wave");
   static_assert(WSLOT % 1024 == 0 && LDS <= 160 * 1024, "LDS");
+};
+
+// conv_res_pair_h3's geometry: RpGeom's rows and wave layout, h3 images (8 pieces of 16 B per row
+// and 32-channel chunk: 4 B per element), so taller tiles fit the LDS
+template <int C>
+constexpr int kRp3Rows = C == 32 ? 624 : 240;
+template <int C, int RR = kRp3Rows<C>>
+struct RpGeom3 {
+  static constexpr int R = RR;
+  static constexpr int M1 = R + 16, H1 = 32, NS = M1 + 2 * H1;
+  static constexpr int WC = C / 32, WR = 8 / WC;
+  static constexpr int NB1 = M1 / 16, RB1 = NB1 / WR;
+  static constexpr int NB2 = R / 16, RB2 = (NB2 + WR - 1) / WR;
+  static constexpr int PS = NS * 16;
+  static constexpr int NCH = C / 32;            // K32 chunks per tap
+  static constexpr int IMG = NCH * 8 * PS;      // S image bytes (T reuses it)
+  static constexpr int WTAP = C * C * 4;        // one tap of h3 weights (bytes)
+  static constexpr int G8 = C / 8;
+  static constexpr int NIT = (NS * G8 + 511) / 512;
+  static_assert(NB1 % WR == 0 && RB1 == RB2, "row blocks per wave");
+  static_assert(IMG + 2 * kMaxGroup * C * 4 <= 160 * 1024, "LDS");
 };
 
 }  // namespace
@@ -698,6 +720,284 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_g(const ResPairParams p)
 #endif
 }
 
+// conv_res_pair_h3 (round 5): conv_res_pair_g in h3 arithmetic (ResPairParams::h3; the fp16 h / l
+// split of conv_gemm_x3dq, three products per fp32 product on v_mfma_f32_16x16x32_f16).  A K32 chunk
+// of a tap is three MFMAs per 16 x 16 block, W{h'} . X{l}, W{l'} . X{h}, W{h'} . X{h}, the lanes of K
+// group kg = lane >> 4 holding channel group kg of both operands: half the MFMAs of x6, two fragment
+// reads per block and chunk instead of six, and images of 4 B per element instead of 6 (byte
+// ((chunk * 8 + piece) * NS + row) * 16, piece = plane * 4 + channel group).  Weights: the
+// ConvParams::w3 tap slices ([chunk][Cout][4][h' 8 | l' 8], scaled by 2^w3_shift per conv); the
+// accumulators are scaled back before the bias.  Schedule, tiles and hand-offs are conv_res_pair_g's.
+template <int C, bool MEAN, int RR = kRp3Rows<C>>
+__global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p) {
+  using G = RpGeom3<C, RR>;
+  constexpr int R = G::R, WR = G::WR, RB = G::RB1, PS = G::PS;
+  constexpr int G8 = G::G8, NIT = G::NIT, NS = G::NS;
+  constexpr int NCH = G::NCH, IMG = G::IMG, WTAP = G::WTAP;
+  __shared__ __attribute__((aligned(16))) char lds[IMG + 2 * kMaxGroup * C * 4];
+  float* const bias_lds = reinterpret_cast<float*>(lds + IMG);  // [conv][member][C]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wc = wave % G::WC, wr = wave / G::WC;
+  const int l15 = lane & 15, kg = lane >> 4;
+  const int L = p.L, nmem = p.nmem;
+  const int ntl = (L + R - 1) / R;
+  const int total = ntl * p.batch;
+
+  // ---- S image fill (as conv_res_pair) ----
+  f32x4 pf[NIT][2];
+  auto issue_fill_item = [&](const float* src, int r0, int k) {
+    const int it = min(tid + 512 * k, NS * G8 - 1);
+    const int s = ((it >> 3) / G8) * 8 + (it & 7), g8 = (it >> 3) % G8;
+    const int a = min(max(r0 - 8 - G::H1 + s, 0), L - 1);
+    const f32x4* q = reinterpret_cast<const f32x4*>(src + (long long)a * C + g8 * 8);
+    pf[k][0] = q[0];
+    pf[k][1] = q[1];
+  };
+  auto commit_fill = [&](int r0) {
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int it = tid + 512 * k;
+      if (!(NIT * 512 == NS * G8 || it < NS * G8)) continue;
+      const int s = ((it >> 3) / G8) * 8 + (it & 7), g8 = (it >> 3) % G8;
+      const int a = r0 - 8 - G::H1 + s;
+      const bool ok = a >= 0 && a < L;
+      s16x8 hv, lv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sv = rp_silu(pf[k][e >> 2][e & 3]);
+        const float v = ok ? sv : 0.f;
+        unsigned short hh, ll;
+        split2h(v, hh, ll);
+        hv[e] = (short)hh;
+        lv[e] = (short)ll;
+      }
+      char* d = lds + ((g8 >> 2) * 8 + (g8 & 3)) * PS + s * 16;
+      *reinterpret_cast<s16x8*>(d) = hv;
+      *reinterpret_cast<s16x8*>(d + 4 * PS) = lv;
+    }
+  };
+
+  // ---- weight fragments of chunk ch of a tap ([chunk][Cout][128 B], the ConvParams::w3 tap slice):
+  // [column block][h' | l'] of the lane's channel group ----
+  s16x8 wf[NCH][2][2];
+  const int wo0 = ((2 * wc) * 16 + l15) * 128 + kg * 32, wo1 = wo0 + 16;
+  auto load_wf = [&](const unsigned short* wtap, int ch) {
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)wtap, 0, WTAP, 0x00020000);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int so = (ch * C + cb * 16) * 128;
+      wf[ch][cb][0] = __builtin_bit_cast(s16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, wo0, so, 0));
+      wf[ch][cb][1] = __builtin_bit_cast(s16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, wo1, so, 0));
+    }
+  };
+  // the tap after tap j of conv `conv` of member m: the stream runs c1, c2 of each member, then
+  // member 0 again (the next tile; past the last tile harmless loads of weights already used)
+  auto next_tap = [&](int m, int conv, int j) -> const unsigned short* {
+    if (j + 1 < p.taps[m]) return (conv ? p.w2[m] : p.w1[m]) + (long long)(j + 1) * (WTAP / 2);
+    if (conv == 0) return p.w2[m];
+    return p.w1[m + 1 < nmem ? m + 1 : 0];
+  };
+
+  // ---- one tap, chunk-major: the MFMAs of chunk ch for every row block of the wave, then chunk ch
+  // of the next tap into the fragment registers; hook() once every reload of the tap is issued (its
+  // loads are then younger than the fragments the next tap waits for) ----
+  // lane parts of the two activation reads (h and l pieces of the lane's channel group, row within
+  // the 16-row block); a tap adds its wave-uniform row offset once, row block / chunk offsets are
+  // instruction immediates
+  const int pkh = (kg * NS + l15) * 16, pkl = ((4 + kg) * NS + l15) * 16;
+  auto tap = [&](f32x4 (&acc)[RB][2], int rowoff, int nrb, const unsigned short* wnext, auto hook) {
+    const int tb = (wr * 16 + rowoff) * 16;
+    const char *xbh = lds + pkh + tb, *xbl = lds + pkl + tb;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        if (i < nrb) {
+          const int io = (WR * 16 * i) * 16 + ch * 8 * PS;
+          const s16x8 xl = *reinterpret_cast<const s16x8*>(xbl + io);
+          const s16x8 xh = *reinterpret_cast<const s16x8*>(xbh + io);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) {
+            acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, wf[ch][cb][0]),
+                                                                __builtin_bit_cast(f16x8, xl), acc[i][cb], 0, 0, 0);
+            acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, wf[ch][cb][1]),
+                                                                __builtin_bit_cast(f16x8, xh), acc[i][cb], 0, 0, 0);
+            acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, wf[ch][cb][0]),
+                                                                __builtin_bit_cast(f16x8, xh), acc[i][cb], 0, 0, 0);
+          }
+        }
+      }
+      load_wf(wnext, ch);
+      // keep the reloads here: left to itself the scheduler sinks all of them to the end of the tap,
+      // and the next tap's first MFMAs then wait a whole L2 round trip
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    hook();
+  };
+  auto no_hook = [] {};
+
+  const int nrb2 = min(RB, (G::NB2 - wr + WR - 1) / WR);
+  int tile = blockIdx.x;
+  if (tile >= total) return;  // whole workgroup, before any barrier
+  int b = tile / ntl, r0 = (tile - b * ntl) * R;
+  if (tid < 2 * nmem * C) {
+    const int conv = tid / (nmem * C), m = (tid / C) % nmem, c = tid % C;
+    bias_lds[(conv * kMaxGroup + m) * C + c] = (conv ? p.b2[m] : p.b1[m])[c];
+  }
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) load_wf(p.w1[0], ch);
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) issue_fill_item(p.src[0] + (long long)b * p.bstride, r0, k);
+  commit_fill(r0);
+  rp_barrier();
+  f32x4 macc[MEAN ? RB : 1][2];
+#ifdef RP_DIAG_STAMPS
+  unsigned long long dg[16] = {};
+#endif
+  for (;;) {
+    const int next_tile = tile + gridDim.x;
+    const bool more = next_tile < total;
+    const int nb = more ? next_tile / ntl : 0, nr0 = more ? (next_tile - nb * ntl) * R : 0;
+    for (int m = 0; m < nmem; ++m) {
+      const int k = p.taps[m], hk = (k - 1) >> 1, d = p.dil[m];
+      const long long cb0 = (long long)b * p.bstride;
+      const bool last_m = m + 1 == nmem;
+      const bool has_next = !last_m || more;
+      f32x4 acc[RB][2];
+      RP_T(ta);
+      // ---- c1 over rows [r0 - 8, r0 + R + 8) from the S image
+#pragma unroll
+      for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int ts = p.tap_sync;
+      for (int j = 0; j < k; ++j) {
+        tap(acc, G::H1 + (j - hk) * d, RB, next_tap(m, 0, j), no_hook);
+        if (ts && (j + 1) % ts == 0 && j + 1 < k) rp_barrier();  // workgroup-uniform
+      }
+      RP_T(tb);
+      rp_barrier();  // every wave's S reads are done before T overwrites them
+      // ---- T image: silu(c1 + b1) as h / l over the S image (zero outside the clip)
+      const float us1 = __builtin_ldexpf(1.0f, -p.w3_shift1[m]);
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(bias_lds + m * C + c0);
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int ir = (wr + WR * i) * 16 + l15, a = r0 - 8 + ir;
+          const bool ok = a >= 0 && a < L;
+          s16x4 hv, lv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float sv = rp_silu(acc[i][cb][e] * us1 + bias[e]);
+            const float v = ok ? sv : 0.f;
+            unsigned short hh, ll;
+            split2h(v, hh, ll);
+            hv[e] = (short)hh;
+            lv[e] = (short)ll;
+          }
+          char* dst = lds + ((c0 >> 5) * 8 + ((c0 >> 3) & 3)) * PS + ir * 16 + (c0 & 7) * 2;
+          *reinterpret_cast<s16x4*>(dst) = hv;
+          *reinterpret_cast<s16x4*>(dst + 4 * PS) = lv;
+        }
+      }
+      rp_barrier();
+      RP_T(tc);
+      // ---- c2 over rows [r0, r0 + R) from the T image.  Tap 0 loads the residual rows, taps 1 and 2
+      // the next S image's rows (this tile's next ResBlock, or the next tile's first), each after the
+      // tap's fragment reloads (k >= 3, so taps 0..2 exist; they are peeled so that the register
+      // arrays are indexed by constants)
+#pragma unroll
+      for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* nsrc = !last_m ? p.src[m + 1] + cb0 : p.src[0] + (long long)nb * p.bstride;
+      const int nsr0 = !last_m ? r0 : nr0;
+      f32x4 res[RB][2];
+      auto res_hook = [&] {
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int q = min(r0 + (wr + WR * i) * 16 + l15, L - 1);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) {
+            const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+            res[i][cb] = *reinterpret_cast<const f32x4*>(p.src[m] + cb0 + (long long)q * C + c0);
+          }
+        }
+      };
+      auto pf_hook0 = [&] {
+        if (!has_next) return;
+#pragma unroll
+        for (int kk = 0; kk < NIT / 2; ++kk) issue_fill_item(nsrc, nsr0, kk);
+      };
+      auto pf_hook1 = [&] {
+        if (!has_next) return;
+#pragma unroll
+        for (int kk = NIT / 2; kk < NIT; ++kk) issue_fill_item(nsrc, nsr0, kk);
+      };
+      tap(acc, 8 - hk, nrb2, next_tap(m, 1, 0), res_hook);
+      if (ts == 1) rp_barrier();
+      tap(acc, 9 - hk, nrb2, next_tap(m, 1, 1), pf_hook0);
+      if (ts && 2 % ts == 0) rp_barrier();
+      tap(acc, 10 - hk, nrb2, next_tap(m, 1, 2), pf_hook1);
+      if (ts && 3 % ts == 0 && 3 < k) rp_barrier();
+      for (int j = 3; j < k; ++j) {
+        tap(acc, 8 + j - hk, nrb2, next_tap(m, 1, j), no_hook);
+        if (ts && (j + 1) % ts == 0 && j + 1 < k) rp_barrier();
+      }
+      RP_T(te);
+      // ---- epilogue: state + c2 + b2 (rows past the clip end are dropped)
+      const float us2 = __builtin_ldexpf(1.0f, -p.w3_shift2[m]);
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(bias_lds + (kMaxGroup + m) * C + c0);
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          if (i >= nrb2) break;
+          const int q = r0 + (wr + WR * i) * 16 + l15;
+          const f32x4 v = res[i][cb] + (acc[i][cb] * us2 + bias);
+          if constexpr (!MEAN) {
+            if (q < L) *reinterpret_cast<f32x4*>(p.dst[m] + cb0 + (long long)q * C + c0) = v;
+          } else if (m == 0) {
+            macc[i][cb] = v;
+          } else if (!last_m) {
+            macc[i][cb] = macc[i][cb] + v;
+          } else {
+            const f32x4 mv = (macc[i][cb] + v) / 3.0f;
+            f32x4 sv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sv[e] = rp_silu(mv[e]);
+            if (q < L) *reinterpret_cast<f32x4*>(p.mean_out + cb0 + (long long)q * C + c0) = sv;
+          }
+        }
+      }
+      RP_T(tf);
+      if (has_next) {
+        rp_barrier();  // every wave's T reads are done before the next S image overwrites them
+        commit_fill(nsr0);
+        rp_barrier();
+      }
+#ifdef RP_DIAG_STAMPS
+      {
+        RP_T(tg);
+        dg[0] += tb - ta; dg[1] += tc - tb; dg[2] += te - tc; dg[3] += tf - te; dg[4] += tg - tf;
+        dg[5] += 1; dg[6] += k; dg[7] += k;
+      }
+#endif
+    }
+    if (!more) break;
+    tile = next_tile;
+    b = nb;
+    r0 = nr0;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last tap's (unused) fragment reloads
+#ifdef RP_DIAG_STAMPS
+  (void)dg;
+#endif
+}
+
+
 // conv_res_pair_w4 (round 5): the barrier-free tap loops of conv_res_pair_g on 4-wave workgroups, TWO
 // per CU.  In the 8-wave kernels the two waves of a SIMD belong to one workgroup and go through the
 // same phases together: both run their tap loops (sharing the matrix pipe, each covering the other's
@@ -974,14 +1274,16 @@ hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** k
   // C = 32: the barrier-free conv_res_pair_g, C = 64: the step schedule; Knobs (A/B and
   // tests): rp_old runs the step schedule at C = 32 too, rp_g64 the barrier-free kernel at C = 64,
   // rp_w4 conv_res_pair_w4 (two 4-wave workgroups per CU: same bits, measured 2-6 % slower)
-  const bool w4 = kn.rp_w4 && !kn.rp_old && !kn.rp_g64;
+  const bool w4 = kn.rp_w4 && !kn.rp_old && !kn.rp_g64 && !p.h3;
   const int slots = w4 ? 2 * cus : cus;
   // rows per tile: the default unless a smaller tile finishes the launch sooner, by rounds of tiles
   // over the workgroup slots times a tile's rows (c1 rows R + 16, c2 rows R, ~64 rows' worth of fixed
   // cost); Knobs::rp_rows forces one of the instantiated sizes.  Every size gives the same bits.
   static constexpr int kW8_32[3] = {496, 240, 112}, kW8_64[3] = {176, 112, 48};
+  static constexpr int kH3_32[3] = {624, 240, 112}, kH3_64[3] = {240, 112, 48};
   static constexpr int kW4_32[3] = {304, 112, 48}, kW4_64[3] = {112, 48, 48};
-  const int* sizes = w4 ? (p.C == 32 ? kW4_32 : kW4_64) : (p.C == 32 ? kW8_32 : kW8_64);
+  const int* sizes = p.h3 ? (p.C == 32 ? kH3_32 : kH3_64)
+                     : w4 ? (p.C == 32 ? kW4_32 : kW4_64) : (p.C == 32 ? kW8_32 : kW8_64);
   int si = 0;
   long long best = -1;
   for (int i = 0; i < 3; ++i) {
@@ -1015,7 +1317,10 @@ hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** k
     else if (si == 1) DCX_RP_GO(KERN, CC, R1, ",small");       \
     else DCX_RP_GO(KERN, CC, R2, ",small");                    \
   } while (0)
-  if (w4) {
+  if (p.h3) {  // h3 weights: conv_res_pair_h3 (the barrier-free schedule at both widths)
+    if (p.C == 32) DCX_RP_SIZES(conv_res_pair_h3, 32, 624, 240, 112);
+    else DCX_RP_SIZES(conv_res_pair_h3, 64, 240, 112, 48);
+  } else if (w4) {
     if (p.C == 32) DCX_RP_SIZES(conv_res_pair_w4, 32, 304, 112, 48);
     else DCX_RP_SIZES(conv_res_pair_w4, 64, 112, 48, 48);
   } else if (p.C == 32 && !kn.rp_old) {

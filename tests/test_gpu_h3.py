@@ -166,3 +166,34 @@ def test_conv_pre_h3(eng, state, cfg):
     e6, e3 = _rel(y6, ref), _rel(y3, ref)
     print(f"\nconv_pre rel err: x6 {e6:.3g}, h3 {e3:.3g}")
     assert e3 < 2e-5 and e3 < 4 * max(e6, 1e-7)
+
+
+@pytest.mark.parametrize("stage", [3, 4])
+def test_pair_kernels_h3_vs_oracle(eng, state, cfg, stage):
+    """The C = 64 / 32 ParallelBlocks on conv_res_pair_h3 (Knobs::h3_pairs) against the fp64 oracle,
+    as the x6 pair kernels."""
+    from oracle import reference_cpu as R
+
+    C = cfg["decoder"]["upsample_initial_channel"] >> (stage + 1)
+    x = torch.from_numpy(np.random.default_rng(30 + stage).standard_normal((2, C, 1000)).astype(np.float32))
+    ref = torch.nn.functional.silu(R.parallel_block(x.double(), state["generator"], stage, cfg["decoder"], torch.float64))
+    ref = ref.numpy()
+    with eng.knobs(DCX_H3_PAIRS=0):
+        y6 = eng.module(f"generator.resblocks.{stage}", _cl(x.numpy())).cpu().numpy().transpose(0, 2, 1)
+    with eng.knobs(DCX_H3_PAIRS=1):
+        y3 = eng.module(f"generator.resblocks.{stage}", _cl(x.numpy())).cpu().numpy().transpose(0, 2, 1)
+    e6, e3 = _rel(y6, ref), _rel(y3, ref)
+    print(f"\nstage {stage} (C = {C}) pairs: x6 rel err {e6:.3g}, h3 rel err {e3:.3g}")
+    assert e3 < 2e-4 and e3 < 4 * max(e6, 1e-7)
+    assert not np.array_equal(y3, y6)
+
+
+def test_generator_h3_pairs_vs_x6(eng, golden):
+    g = golden["e2e_batch"]
+    z = torch.from_numpy(g["quantized"]).transpose(1, 2)
+    with eng.knobs(DCX_H3=0, DCX_H3_1X1=0, DCX_H3_PAIRS=0):
+        w6 = eng.generate(z).cpu().numpy()
+    w3 = eng.generate(z).cpu().numpy()
+    s36, s3r = _snr(w3, w6), _snr(w3, g["wav"])
+    print(f"\nh3 + h3 pairs: vs x6 {s36:.1f} dB, vs reference {s3r:.1f} dB")
+    assert s36 >= 100 and s3r >= 80

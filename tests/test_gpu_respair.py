@@ -88,10 +88,11 @@ def test_pair_kernels_same_bits(engines, B, T):
     loop and the weight stream's wrap-around past the last tile)."""
     fused, _ = engines
     z = _z(B, T, 300 + T)
-    a = fused.generate(z)
+    with fused.knobs(DCX_H3_PAIRS=0):  # the x6 pair kernels (h3: conv_res_pair_h3, the default)
+        a = fused.generate(z)
     outs = []
     for kn in ({"DCX_RP_W4": 1}, {"DCX_RP_OLD": 1}, {"DCX_RP_G64": 1}):
-        with fused.knobs(**kn):
+        with fused.knobs(DCX_H3_PAIRS=0, **kn):
             outs.append(fused.generate(z))
     torch.cuda.synchronize()
     assert torch.isfinite(a).all()
@@ -111,9 +112,17 @@ def test_tile_rows_same_bits(engines, B, T):
     outs = []
     for r in (304, 496, 240, 112, 176, 48):
         for kn in ({}, {"DCX_RP_W4": 1}, {"DCX_RP_OLD": 1}):
-            with fused.knobs(DCX_RP_R=r, **kn):
+            with fused.knobs(DCX_H3_PAIRS=0, DCX_RP_R=r, **kn):
                 outs.append(fused.generate(z))
     torch.cuda.synchronize()
     assert torch.isfinite(outs[0]).all()
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
+    # conv_res_pair_h3 (the default): 624 / 240 / 112 rows at C = 32, 240 / 112 / 48 at C = 64
+    h3 = [fused.generate(z)]
+    for r in (624, 240, 112, 48):
+        with fused.knobs(DCX_RP_R=r):
+            h3.append(fused.generate(z))
+    torch.cuda.synchronize()
+    for o in h3[1:]:
+        assert torch.equal(h3[0], o)
