@@ -48,7 +48,7 @@ def short(name):
         return f"conv_gemm_x3dq<{bm},{bn},halo>" if parts[1] != "0" else f"conv_gemm_x3dm<{bm},{bn}>"
     if base == "vq_prefilter_b1":
         return "vq_prefilter_b1<256,256>"
-    if base in ("conv_res_pair", "conv_res_pair_g", "conv_res_pair_w4"):  # <C, MEAN, ROWS>
+    if base in ("conv_res_pair", "conv_res_pair_g", "conv_res_pair_w4", "conv_res_pair_h3"):  # <C, MEAN, ROWS>
         return f"{base}<{parts[0]}{',mean' if len(parts) > 1 and parts[1] == 'true' else ''}>"
     if base == "vq_prefilter_dm":  # <XMID>
         return "vq_prefilter_dm<256,256>" if parts and parts[0] == "true" else "vq_prefilter_dm_x2<256,256>"
