@@ -2601,8 +2601,11 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x3dq_group(const ConvGroup g
 // and half by group 1 in MEM1(s) (one tap: group 0 the input pieces, group 1 all weight pieces), so
 // the CU fetches during both segments.  Group 1 may overwrite step s's slot only once all four of its
 // waves have read their step-s fragments: each wave, once its reads have returned, bumps an LDS
-// counter, and waits for it to reach 4 (s + 1) before issuing.  Group 1 retires its pieces at the
-// end of MEM1(s + 1), before the barrier that opens MEM0(s + 1), their first reader.
+// counter, and waits for it to reach 4 (s + 2) before issuing: group 0's waves bump it once too,
+// after their step-0 reads (made before the loop, in segment 0, the segment in which group 1 refills
+// step 0's slot with step 2 -- without them in the count that refill raced those reads and the last
+// clip's output differed between runs, tools/determinism_check.py).  Group 1 retires its pieces at
+// the end of MEM1(s + 1), before the barrier that opens MEM0(s + 1), their first reader.
 template <int HALO, bool SPLIT>
 __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, const int b, const int ph) {
   constexpr int BM = 256, BN = 256, WN = 2, WM = 4;
@@ -2746,6 +2749,10 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
   int cr = 0, mr = 0;
   if (group == 0) {
     readF(0, 0, 0);
+    if (SPLIT) {  // step 0's slot is refilled by group 1 in segment 0: count these reads too
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(rd_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     adv(cr, mr);
     for (int s = 0; s < nsteps; ++s) {
       DCX_SEGT(ta);
@@ -2780,7 +2787,7 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
         if (s + 2 < nsteps) {  // this group's pieces of step s + 2, into step s's slot once read
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           if (lane == 0) __hip_atomic_fetch_add(rd_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          const unsigned int want = 4u * (unsigned)(s + 1);
+          const unsigned int want = 4u * (unsigned)(s + 2);  // + group 0's four step-0 reads
           while (__hip_atomic_load(rd_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
           }
           dma_step1(cl, ml, s & 1);

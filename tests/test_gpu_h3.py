@@ -100,6 +100,26 @@ def test_h3_knob_switches_back(eng, golden):
     assert not np.array_equal(a, c)
 
 
+def test_split_issue_same_bits_and_reproducible(eng):
+    """conv_gemm_x3dw's split DMA issue (Knobs::h3_split) changes only who issues the copies: same
+    bits as the unsplit issue, and run-to-run identical (round 5: before group 0's step-0 reads were
+    in the handshake, the last clip of a 32-clip batch differed between runs)."""
+    from distilcodec_nabeel_amd import synth
+
+    n, L = 16, 72000
+    audio = torch.zeros(n, L + 1)
+    for i, c in enumerate(synth.clips(n, L, seed=3, kind="mix")):
+        audio[i, 1:] = torch.from_numpy(c)
+    audio = audio.to("cuda:0")
+    c0, w0 = eng.encode_decode(audio)
+    for _ in range(3):
+        c, w = eng.encode_decode(audio)
+        assert torch.equal(c, c0) and torch.equal(w, w0)
+    with eng.knobs(DCX_H3_SPLIT=0):
+        c, w = eng.encode_decode(audio)
+    assert torch.equal(c, c0) and torch.equal(w, w0)
+
+
 @pytest.mark.parametrize("bn", [0, 256])
 def test_tilings_agree(eng, state, cfg, bn):
     """The 256 x 128 (default) and 128 x 256 tilings sum every output in the same order: same bits."""
