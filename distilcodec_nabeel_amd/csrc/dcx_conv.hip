@@ -497,8 +497,14 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
   };
   // batches of 8 rows (4 when both the residual and the mean accumulator are loaded), halved for
   // 8-channel groups (the same registers)
+  // (the largest batch within the cap that divides the rows per thread: 6 rows -> 3 + 3)
   constexpr int IBF0 = 8 / NH, IBM0 = 4 / NH;
-  constexpr int IBF = ROWS_T < IBF0 ? ROWS_T : IBF0, IBM = ROWS_T < IBM0 ? ROWS_T : IBM0;
+  constexpr auto div_cap = [](int n, int cap) {
+    int d = n < cap ? n : cap;
+    while (n % d) --d;
+    return d;
+  };
+  constexpr int IBF = div_cap(ROWS_T, IBF0), IBM = div_cap(ROWS_T, IBM0);
   static_assert(ROWS_T % IBF == 0 && ROWS_T % IBM == 0, "epilogue batches");
 #pragma unroll 1
   for (int r0 = 0; r0 < BM; r0 += RPP) {
@@ -2606,10 +2612,12 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x3dq_group(const ConvGroup g
 // step 0's slot with step 2 -- without them in the count that refill raced those reads and the last
 // clip's output differed between runs, tools/determinism_check.py).  Group 1 retires its pieces at
 // the end of MEM1(s + 1), before the barrier that opens MEM0(s + 1), their first reader.
-template <int HALO, bool SPLIT>
+// BN = 256: 256 x 256 tiles of 64 x 128 wave tiles (Cout % 256 == 0); BN = 128: 384 x 128 tiles of
+// 48 x 128 wave tiles (the C = 128 stage: 72 MFMAs per segment against x3dq's 48).
+template <int HALO, bool SPLIT, int BN = 256>
 __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, const int b, const int ph) {
-  constexpr int BM = 256, BN = 256, WN = 2, WM = 4;
-  constexpr int WR = 64, WC = 128, TM = 4, TN = 8;
+  constexpr int BM = BN == 256 ? 256 : 384, WN = BN / 128, WM = 8 / WN;
+  constexpr int WR = BM / WM, WC = 128, TM = WR / 16, TN = WC / 16;
   constexpr int AR = BM + HALO;                 // rows of an input image
   constexpr int A_N = AR / 8, B_N = BN / 8;     // 1 KiB DMA instructions per A chunk / B step
   constexpr int A_PW = A_N / 4;                 // A pieces per group-0 wave
@@ -2830,14 +2838,15 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
   epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
-template <int HALO, bool SPLIT>
+template <int HALO, bool SPLIT, int BN = 256>
 __global__ void __launch_bounds__(512, 2) conv_gemm_x3dw(const ConvParams p) {
+  constexpr int BM = BN == 256 ? 256 : 384;
   int wg, b, ph;
-  flat_tile(((p.Lq + 255) / 256) * (p.Cout / 256), p.batch, wg, b, ph);
-  x3dw_tile<HALO, SPLIT>(p, wg, b, ph);
+  flat_tile(((p.Lq + BM - 1) / BM) * (p.Cout / BN), p.batch, wg, b, ph);
+  x3dw_tile<HALO, SPLIT, BN>(p, wg, b, ph);
 }
 
-template <bool SPLIT>
+template <bool SPLIT, int BN = 256>
 __global__ void __launch_bounds__(512, 2) conv_gemm_x3dw_group(const ConvGroup g) {
   const int t = blockIdx.x;
   const int k = t >= g.start[1] ? (t >= g.start[2] ? 2 : 1) : 0;
@@ -2847,7 +2856,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x3dw_group(const ConvGroup g
   if (k == 0) p = g.p[0];
   else if (k == 1) p = g.p[1];
   else p = g.p[2];
-  x3dw_tile<64, SPLIT>(p, local - b * g.tiles_per_clip[k], b, 0);
+  x3dw_tile<64, SPLIT, BN>(p, local - b * g.tiles_per_clip[k], b, 0);
 }
 
 // Whether conv_gemm_x3dq<bn> (taps >= 3 with a halo) or conv_gemm_x3dm<bn> (one tap) takes an h3
@@ -2869,9 +2878,11 @@ static bool x3dq_ok(const ConvParams& p, int bn, bool wide = false) {
 // against 128 x 256: half the weight DMA per step, C2 205.1 -> 193.2 ms, r05i.)  Knobs::h3_bn
 // (DCX_H3_BN, A/B): 128 = the 256 x 128 tiles everywhere, 256 = the 128 x 256 ones at Cout % 256 == 0.
 // Returns the column tile, 512 standing for the 256 x 256 kernel.
+// 384 stands for the 384 x 128 conv_gemm_x3dw (Cout % 256 != 0, taps >= 2; DCX_H3_BN=128 keeps the
+// 256 x 128 conv_gemm_x3dq there).
 static int x3dq_bn(const ConvParams& p) {
   const int k = p.kn ? p.kn->h3_bn : 0;
-  if (p.Cout % 256) return 128;
+  if (p.Cout % 256) return k == 128 || p.taps < 2 ? 128 : 384;
   return k == 128 ? 128 : k == 256 ? 256 : 512;
 }
 
@@ -4417,7 +4428,17 @@ hipError_t launch_conv(const ConvParams& p, int batch, int phases, hipStream_t s
   if (p.Cin % BK || p.Cout % 32 || phases < 1 || phases > kMaxPhases) return hipErrorInvalidValue;
   if (p.x_compact == 3) {  // h2 input: the h3 kernels only
     const int bn = x3dq_bn(p);
-    if (!x3dq_ok(p, bn == 512 ? 256 : bn, bn == 512)) return hipErrorInvalidValue;
+    if (!x3dq_ok(p, bn == 512 ? 256 : bn == 384 ? 128 : bn, bn >= 384)) return hipErrorInvalidValue;
+    if (bn == 384) {  // 384 x 128 tiles (the C = 128 stage)
+      const dim3 grid((unsigned)(((p.Lq + 383) / 384) * (p.Cout / 128) * batch * phases));
+      ConvParams q = p;
+      q.batch = batch;
+      q.phases = phases;
+      if (kname) *kname = "conv_gemm_x3dw<384,128,halo>";
+      if (knobs(p).h3_split) hipLaunchKernelGGL((conv_gemm_x3dw<64, true, 128>), grid, dim3(512), 0, s, q);
+      else hipLaunchKernelGGL((conv_gemm_x3dw<64, false, 128>), grid, dim3(512), 0, s, q);
+      return hipGetLastError();
+    }
     if (bn == 512) {
       const dim3 grid((unsigned)(((p.Lq + 255) / 256) * (p.Cout / 256) * batch * phases));
       ConvParams q = p;
@@ -4563,9 +4584,12 @@ hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t
   if (n < 1 || n > kMaxGroup || batch < 1) return hipErrorInvalidValue;
   const int cout = ps[0].Cout;
   if (ps[0].x_compact == 3) {  // h3 convs: conv_gemm_x3dw_group / x3dq_group (any tile count)
-    const int bsel = x3dq_bn(ps[0]), bn = bsel == 512 ? 256 : bsel, bm = bsel == 512 ? 256 : 32768 / bn;
+    const int bsel = x3dq_bn(ps[0]);
+    const int bn = bsel == 512 ? 256 : bsel == 384 ? 128 : bsel, bm = bsel == 512 ? 256 : bsel == 384 ? 384 : 32768 / bn;
     for (int i = 0; i < n; ++i)
-      if (ps[i].Cout != cout || ps[i].x_compact != 3 || ps[i].taps < 3 || !x3dq_ok(ps[i], bn)) return hipErrorNotSupported;
+      if (ps[i].Cout != cout || ps[i].x_compact != 3 || ps[i].taps < 3 || x3dq_bn(ps[i]) != bsel ||
+          !x3dq_ok(ps[i], bn, bsel >= 384))
+        return hipErrorNotSupported;
     int order[kMaxGroup] = {0, 1, 2};
     for (int i = 0; i < n; ++i)
       for (int j = i + 1; j < n; ++j)
@@ -4581,7 +4605,11 @@ hipError_t launch_conv_group(const ConvParams* ps, int n, int batch, hipStream_t
     }
     if (start > (1LL << 30)) return hipErrorInvalidValue;
     for (int k = n; k <= kMaxGroup; ++k) g.start[k] = (int)start;
-    if (bsel == 512) {
+    if (bsel == 384) {
+      if (kname) *kname = "conv_gemm_x3dw_group<384,128,halo>";
+      if (knobs(ps[0]).h3_split) hipLaunchKernelGGL((conv_gemm_x3dw_group<true, 128>), dim3((unsigned)start), dim3(512), 0, s, g);
+      else hipLaunchKernelGGL((conv_gemm_x3dw_group<false, 128>), dim3((unsigned)start), dim3(512), 0, s, g);
+    } else if (bsel == 512) {
       if (kname) *kname = "conv_gemm_x3dw_group<256,256,halo>";
       if (knobs(ps[0]).h3_split) hipLaunchKernelGGL(conv_gemm_x3dw_group<true>, dim3((unsigned)start), dim3(512), 0, s, g);
       else hipLaunchKernelGGL(conv_gemm_x3dw_group<false>, dim3((unsigned)start), dim3(512), 0, s, g);

@@ -120,14 +120,15 @@ def test_split_issue_same_bits_and_reproducible(eng):
     assert torch.equal(c, c0) and torch.equal(w, w0)
 
 
-@pytest.mark.parametrize("bn", [0, 256])
-def test_tilings_agree(eng, state, cfg, bn):
-    """The 256 x 128 (default) and 128 x 256 tilings sum every output in the same order: same bits."""
-    C = cfg["decoder"]["upsample_initial_channel"] >> 1
-    x = torch.from_numpy(np.random.default_rng(5).standard_normal((1, C, 700)).astype(np.float32))
-    ref = eng.module("generator.resblocks.0", _cl(x.numpy())).cpu().numpy()
+@pytest.mark.parametrize("stage,bn", [(0, 128), (0, 256), (2, 128)])
+def test_tilings_agree(eng, state, cfg, stage, bn):
+    """Every h3 tiling (x3dw 256 x 256 / 384 x 128 by default, x3dq 256 x 128 and 128 x 256 with
+    DCX_H3_BN) sums every output in the same order: same bits."""
+    C = cfg["decoder"]["upsample_initial_channel"] >> (stage + 1)
+    x = torch.from_numpy(np.random.default_rng(5).standard_normal((1, C, 900)).astype(np.float32))
+    ref = eng.module(f"generator.resblocks.{stage}", _cl(x.numpy())).cpu().numpy()
     with eng.knobs(DCX_H3_BN=bn):
-        y = eng.module("generator.resblocks.0", _cl(x.numpy())).cpu().numpy()
+        y = eng.module(f"generator.resblocks.{stage}", _cl(x.numpy())).cpu().numpy()
     assert np.array_equal(y, ref)
 
 

@@ -37,10 +37,11 @@ def short(name):
         return f"{base}<{65536 // int(parts[0])},{parts[0]},halo>"
     if base == "conv_gemm_x6dq":  # <BN>, halo
         return f"{base}<{65536 // int(parts[0])},{parts[0]},halo>"
-    if base == "conv_gemm_x3dw_group":
-        return "conv_gemm_x3dw_group<256,256,halo>"
-    if base == "conv_gemm_x3dw":  # <HALO>
-        return "conv_gemm_x3dw<256,256,halo>" if parts and parts[0] != "0" else "conv_gemm_x3dw<256,256>"
+    if base == "conv_gemm_x3dw_group":  # <SPLIT[, BN]>
+        return "conv_gemm_x3dw_group<384,128,halo>" if len(parts) > 1 and parts[1] == "128" else "conv_gemm_x3dw_group<256,256,halo>"
+    if base == "conv_gemm_x3dw":  # <HALO, SPLIT[, BN]>
+        tile = "384,128" if len(parts) > 2 and parts[2] == "128" else "256,256"
+        return f"conv_gemm_x3dw<{tile},halo>" if parts and parts[0] != "0" else f"conv_gemm_x3dw<{tile}>"
     if base == "conv_gemm_x3dq_group":  # <BN>, halo
         return f"{base}<{32768 // int(parts[0])},{parts[0]},halo>"
     if base == "conv_gemm_x3dq":  # <BN, HALO>; HALO = 0: the one-tap conv_gemm_x3dm
