@@ -728,10 +728,11 @@ bool takes_compact(const dcx_codec* h, const ConvW& w, long long rows) {
          rows < (1LL << 31) && dcx::bf16dm_takes(w.cin, w.cout, (int)rows, w.cin, 1);
 }
 
-// Whether a generator conv with a tap halo (conv_pre, the wide ConvTs) runs in h3 arithmetic
-// (conv_gemm_x3dw; Knobs::h3, x6 mode, not in the split-K latency mode), so its producer writes h2.
+// Whether a generator conv with a tap halo (conv_pre, the ConvTs with Cout % 128 == 0) runs in h3
+// arithmetic (conv_gemm_x3dw; Knobs::h3, x6 mode, not in the split-K latency mode), so its producer
+// writes h2.
 bool takes_h3_conv(const dcx_codec* h, const ConvW& w) {
-  return h->knobs.h3 && h->gemm_mode == DCX_GEMM_X6 && h->split_k < 2 && w.w3 && w.taps >= 2 && w.cout % 256 == 0;
+  return h->knobs.h3 && h->gemm_mode == DCX_GEMM_X6 && h->split_k < 2 && w.w3 && w.taps >= 2 && w.cout % 128 == 0;
 }
 
 // Whether a one-tap conv runs in h3 arithmetic (conv_gemm_x3dm; Knobs::h3_1x1, x6 mode, not in the
@@ -2059,12 +2060,13 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
   if (with_generator) {
     const std::string g = "generator.";
     int ch = c.gen_channels;
-    // h3 weights for the convs conv_gemm_x3dw takes (Cout % 256 == 0, two taps or more)
+    // h3 weights for the convs conv_gemm_x3dw takes (Cout % 256 == 0, or Cout % 128 == 0 on its
+    // 384 x 128 tiles; two taps or more)
     h->conv_pre = B.conv(g + "conv_pre", c.vq_dim, ch, c.gen_pre_k, 1, (c.gen_pre_k - 1) / 2, true,
                          ch % 256 == 0 && c.gen_pre_k >= 2);
     for (int i = 0; i < c.n_ups; ++i) {
       h->ups[i] = B.convT(g + "ups." + std::to_string(i), ch, ch / 2, c.up_kernels[i], c.up_rates[i],
-                          (ch / 2) % 256 == 0 && c.up_kernels[i] / c.up_rates[i] >= 2);
+                          (ch / 2) % 128 == 0 && c.up_kernels[i] / c.up_rates[i] >= 2);
       ch /= 2;
       for (int rb = 0; rb < c.n_res; ++rb) {
         const int k = c.res_kernels[rb];

@@ -2879,10 +2879,10 @@ static bool x3dq_ok(const ConvParams& p, int bn, bool wide = false) {
 // (DCX_H3_BN, A/B): 128 = the 256 x 128 tiles everywhere, 256 = the 128 x 256 ones at Cout % 256 == 0.
 // Returns the column tile, 512 standing for the 256 x 256 kernel.
 // 384 stands for the 384 x 128 conv_gemm_x3dw (Cout % 256 != 0, taps >= 2; DCX_H3_BN=128 keeps the
-// 256 x 128 conv_gemm_x3dq there).
+// 256 x 128 conv_gemm_x3dq there where it can, taps >= 3).
 static int x3dq_bn(const ConvParams& p) {
   const int k = p.kn ? p.kn->h3_bn : 0;
-  if (p.Cout % 256) return k == 128 || p.taps < 2 ? 128 : 384;
+  if (p.Cout % 256) return (k == 128 && p.taps >= 3) || p.taps < 2 ? 128 : 384;
   return k == 128 ? 128 : k == 256 ? 256 : 512;
 }
 

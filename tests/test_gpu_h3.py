@@ -156,10 +156,10 @@ def test_convnext_block_h3_vs_oracle(eng, golden, state):
     assert not np.array_equal(y3, y6)  # the h3 path ran
 
 
-@pytest.mark.parametrize("i", [0, 1])
+@pytest.mark.parametrize("i", [0, 1, 2])
 def test_wide_conv_transpose_h3(eng, golden, i):
-    """ups[0] / ups[1] (Cout 512 / 256, 2 / 3 polyphase taps) on conv_gemm_x3dw against the
-    reference's fixture, as the x6 path."""
+    """ups[0] / ups[1] / ups[2] (Cout 512 / 256 / 128, 2 / 3 / 2 polyphase taps) on conv_gemm_x3dw
+    (256 x 256 tiles, 384 x 128 for Cout 128) against the reference's fixture, as the x6 path."""
     m = golden["modules"]
     x = _cl(m[f"ups{i}_in"])
     with eng.knobs(DCX_H3=0):
