@@ -1039,7 +1039,7 @@ int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, in
 int run_ln(dcx_codec* h, const LnW& l, const float* x, Act y, long long rows, hipStream_t s, bool bf16_in = false) {
   const int form = bf16_in && h->gemm_mode == DCX_GEMM_BF16 ? 2 : 1;
   LAUNCH(h, s, "ln_rows", 8.0 * rows * l.C, 8.0 * rows * l.C,
-         dcx::launch_ln_rows(x, y.f, y.p, y.p && y.c1 ? 1 : 0, l.w, l.b, rows, l.C, 1e-6f, form, s));
+         dcx::launch_ln_rows(x, y.f, y.p, y.p && y.c1 ? 1 : y.p && y.h2 ? 3 : 0, l.w, l.b, rows, l.C, 1e-6f, form, s));
   return DCX_OK;
 }
 
@@ -1090,6 +1090,7 @@ int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipSt
   for (int i = 0; i < 4; ++i) {
     if (i > 0) {
       ln.c1 = ln.p && takes_compact(h, h->ds_conv[i], M);
+      ln.h2 = ln.p && takes_h3(h, h->ds_conv[i]);  // the downsample 1x1 conv on conv_gemm_x3dw
       RUN(run_ln(h, h->ds_ln[i], xb, ln, M, s));
       ConvCall cd = pointwise(ln, M);
       cd.y = xb;
@@ -1628,6 +1629,7 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
     ln.c1 = ln.p && takes_compact(h, h->ds_conv[a], M);
+    ln.h2 = ln.p && takes_h3(h, h->ds_conv[a]);
     RUN(run_ln(h, h->ds_ln[a], x, ln, M, s));
     ConvCall cd = pointwise(ln, M);
     cd.y = y;
@@ -1949,7 +1951,7 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
       if (i > 0) {
         const std::string p = e + "downsample_layers." + std::to_string(i);
         h->ds_ln[i] = B.ln(p + ".0", c.enc_dims[i - 1]);
-        h->ds_conv[i] = B.conv(p + ".1", c.enc_dims[i - 1], c.enc_dims[i], 1, 1, 0);
+        h->ds_conv[i] = B.conv(p + ".1", c.enc_dims[i - 1], c.enc_dims[i], 1, 1, 0, true, true);  // + h3 weights
       }
       h->blocks[i].clear();
       for (int j = 0; j < c.enc_depths[i]; ++j)
