@@ -1229,8 +1229,11 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   cd.y = X;
   RUN(run_conv(h, h->vq_down, cd, s));
   const bool x6c = X6 && takes_compact(h, h->vq_pin, M);
-  RUN(run_block(h, h->vq_down_blk, X, X6, B, T, ln, hid, s, x6c));
-  ConvCall cp = pointwise(CAct(X, X6, x6c), M);
+  const bool h2p = X6 && !x6c && takes_h3(h, h->vq_pin);  // project_in on conv_gemm_x3dw
+  RUN(run_block(h, h->vq_down_blk, X, X6, B, T, ln, hid, s, x6c ? 1 : h2p ? 3 : 0));
+  CAct pin_in(X, X6, x6c);
+  pin_in.h2 = h2p;
+  ConvCall cp = pointwise(pin_in, M);
   cp.y = P;
   cp.y6 = P6;
   cp.y6c = xl;
@@ -1652,7 +1655,7 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
   }
   if (m == "quantizer.grvq.rvqs.0.project_in") {  // residual_vq.py:152
     CAct in(x, nullptr);
-    RUN(ensure_planes(h, in, M, c.vq_dim, ws, s));
+    RUN(ensure_planes(h, in, M, c.vq_dim, ws, s, false, takes_h3(h, h->vq_pin)));
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
     ConvCall cp = pointwise(in, M);
@@ -1967,7 +1970,7 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
     h->vq_down_blk = B.block(q + "downsample.0.1", D);
     h->vq_up = B.convT(q + "upsample.0.0", D, D, 1, 1);
     h->vq_up_blk = B.block(q + "upsample.0.1", D);
-    h->vq_pin = B.conv(q + "grvq.rvqs.0.project_in", D, CD, 1, 1, 0);
+    h->vq_pin = B.conv(q + "grvq.rvqs.0.project_in", D, CD, 1, 1, 0, true, true);  // + h3 weights
     ConvW pout = B.conv(q + "grvq.rvqs.0.project_out", CD, D, 1, 1, 0);
     auto emb = B.need(q + "grvq.rvqs.0.layers.0._codebook.embed", {1, NC, CD});
     if (emb) {
