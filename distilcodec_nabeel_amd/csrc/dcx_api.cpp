@@ -1533,6 +1533,7 @@ int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int3
   Act mel = conv_input(h, ws, (size_t)M * c.n_mels);
   Act feat = conv_input(h, ws, (size_t)M * c.enc_dims[3]);
   feat.c1 = feat.p && takes_compact(h, h->vq_down, M);  // written by the encoder's final LayerNorm
+  feat.h2 = feat.p && !feat.c1 && takes_h3(h, h->vq_down);  // h2 for the quantizer's down conv (x3dw)
   Act z;
   z.f = ws.f((size_t)M * c.vq_dim);
   if (x6_mode(h)) z.p = ws.u16((size_t)M * c.vq_dim * 3);
@@ -1966,7 +1967,7 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
   {
     const std::string q = "quantizer.";
     const int D = c.vq_dim, CD = c.codebook_dim, NC = c.codebook_size;
-    h->vq_down = B.conv(q + "downsample.0.0", D, D, 1, 1, 0);
+    h->vq_down = B.conv(q + "downsample.0.0", D, D, 1, 1, 0, true, true);  // + h3 weights
     h->vq_down_blk = B.block(q + "downsample.0.1", D);
     h->vq_up = B.convT(q + "upsample.0.0", D, D, 1, 1);
     h->vq_up_blk = B.block(q + "upsample.0.1", D);
