@@ -326,7 +326,9 @@ def main():
     ap.add_argument("--no-f32", action="store_true", help="skip the IEEE fp32-MFMA comparison pass at N = 1")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch HIP-event roofline timing")
     ap.add_argument("--gemm", choices=["x6", "f32"], default="x6",
-                    help="x6: fp32 operands as 3 bf16 planes, 6 exact products, f32 accumulate; f32: fp32 MFMA")
+                    help="x6 (DCX_GEMM_X6): fp32-tolerance emulation, h3 (2 fp16 values, 3 products) for the wide "
+                         "generator convs and the ConvNeXt 1x1 convs, x6 (3 bf16 planes, 6 products) elsewhere, fp32 "
+                         "accumulation; f32: IEEE fp32 MFMA")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -420,10 +422,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "arith": ("fp32-accurate: the wide generator convs and the ConvNeXt 1x1 convs as 2 fp16 values per "
-                      "operand (h, l), 3 exact fp16 products per fp32 product (v_mfma_f32_16x16x32_f16, 'h3'); the "
-                      "rest as 3 bf16 planes, 6 exact bf16 products (v_mfma_f32_16x16x32_bf16 / 32x32x16_bf16, 'x6'); "
-                      "fp32 accumulation" if args.gemm == "x6" else "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
+            "arith": ("fp32-tolerance emulation (h3 / x6), not IEEE fp32: the wide generator convs and the ConvNeXt "
+                      "1x1 convs as 2 fp16 values per operand (h, l; 22 significant bits, each operand tensor scaled "
+                      "per clip or row by a power of two from a rigorous bound of its range), 3 exact fp16 products "
+                      "per fp32 product (v_mfma_f32_16x16x32_f16, 'h3'); the rest as 3 bf16 planes (24 bits, the "
+                      "fp32 exponent range), 6 exact bf16 products (v_mfma_f32_16x16x32_bf16 / 32x32x16_bf16, 'x6'); "
+                      "fp32 accumulation; held to the fp32 tolerance of the contract (codes exact on decisive frames, "
+                      ">= 80 dB); the IEEE fp32-MFMA figure is f32_ieee"
+                      if args.gemm == "x6" else "IEEE fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
             "data": "synthetic (speech/music-like 24 kHz clips; seeded synthetic weights, no checkpoint offline)",
             "config": {"workload": workload, "global_batch": n_total, "clip_samples_max": longest,
                        "frames_per_clip": frames, "parallelism": f"clip-sharded x{world}, codes all_gather",

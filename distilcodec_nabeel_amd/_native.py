@@ -94,6 +94,8 @@ SIGNATURES = {
     "dcx_get_gemm_mode": (_I32, [_P]),
     "dcx_set_split_k": (ctypes.c_int, [_P, _I32]),
     "dcx_set_knob": (ctypes.c_int, [_P, ctypes.c_char_p, _I32]),
+    "dcx_get_knob": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.POINTER(_I32)]),
+    "dcx_range_flags": (ctypes.c_int, [_P, ctypes.POINTER(_I32), _I32]),
     "dcx_conv_create": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, ctypes.POINTER(_P)]),
     "dcx_conv_forward": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, _P, _P, _P, _I32, _P]),
     "dcx_conv_destroy": (None, [_P]),
@@ -141,7 +143,7 @@ def lib() -> ctypes.CDLL:
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.dcx_abi_version() != 3:
+    if L.dcx_abi_version() != 4:
         raise NativeUnavailable("libdcx.so ABI version mismatch")
     # A library selected explicitly with DCX_LIB (A/B tooling, diagnostic builds) is taken as is;
     # the in-tree library must have been built from the sources next to it.

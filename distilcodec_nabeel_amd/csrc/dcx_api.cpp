@@ -46,6 +46,9 @@ struct ConvW {
   float* b16 = nullptr;  // the bias rounded to bf16 (bf16 mode: autocast casts it with the weight)
   int cin = 0, cout = 0, taps = 1, phases = 1, in_step = 1, out_mul = 1;
   int in_base[dcx::kMaxPhases] = {0};
+  // h3 activation range (round 6, dcx_kernels.h h2_shift): |out| <= g_abs max|in| + b_abs, g_abs the
+  // largest absolute row sum of the weights over (phase, output channel), b_abs = max |bias|
+  float g_abs = 0.f, b_abs = 0.f;
 };
 
 struct LnW {
@@ -107,6 +110,7 @@ struct dcx_codec {
 
   ConvW vq_down, vq_pin, vq_up;
   BlockW vq_down_blk, vq_up_blk;
+  int* rflag = nullptr;  // device RangeFlag bits (dcx_range_flags; round 6)
   float *codebook = nullptr, *e2 = nullptr, *ptable = nullptr;
   double* e2d = nullptr;          // |e|^2 per code in fp64 (the rescore)
   float emax = 0.f, e2max = 0.f;  // largest codebook row norm / squared norm (prefilter bound)
@@ -449,6 +453,30 @@ struct Builder {
     return w;
   }
 
+  // h3 range bounds of a conv (ConvW::g_abs, b_abs) from its packed fp32 weights [phases][cout][kk]
+  // and its bias
+  static float round_up(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafter(f, INFINITY);
+    return f;
+  }
+  void range_of(ConvW& c, const std::vector<float>& pk, int phases, int cout, size_t kk, const std::string& bias) {
+    if (dry) return;
+    double g = 0;
+    for (int r = 0; r < phases; ++r)
+      for (int o = 0; o < cout; ++o) {
+        double sacc = 0;
+        const float* row = &pk[((size_t)r * cout + o) * kk];
+        for (size_t j = 0; j < kk; ++j) sacc += std::fabs((double)row[j]);
+        g = std::max(g, sacc);
+      }
+    c.g_abs = round_up(g);
+    double bm = 0;
+    if (const HostTensor* t = bias.empty() ? nullptr : find(h, bias))
+      for (float v : t->data) bm = std::max(bm, std::fabs((double)v));
+    c.b_abs = round_up(bm);
+  }
+
   // Conv1d / Linear weight [Cout][Cin][k] -> packed [Cout][k][Cin].
   // h3: also the h3 weights (conv_gemm_x3dq; the generator's ResBlock convs of the wide stages)
   ConvW conv(const std::string& prefix, int cin, int cout, int k, int dil, int pad, bool has_bias = true,
@@ -469,6 +497,7 @@ struct Builder {
       c.b = vec(prefix + ".bias", cout);
       c.b16 = vec_bf16(prefix + ".bias", cout);
     }
+    range_of(c, pk, 1, cout, (size_t)k * cin, has_bias ? prefix + ".bias" : "");
     return c;
   }
 
@@ -494,6 +523,7 @@ struct Builder {
     if (h3 && cin % 32 == 0) c.w3 = h2_pack(pk, s, cout, taps, cin, c.w3_shift);
     c.b = vec(prefix + ".bias", cout);
     c.b16 = vec_bf16(prefix + ".bias", cout);
+    range_of(c, pk, s, cout, (size_t)taps * cin, prefix + ".bias");
     return c;
   }
 
@@ -576,21 +606,62 @@ int max_gen_width(const dcx_config& c) {  // max over generator layers of channe
 // vq_prefilter_bk) instead of planes.
 // h2: p holds the fp16 "h2" layout ([rows][C/32][8][8] h and l; the h3 generator arithmetic,
 // consumer conv_gemm_x3dq).
+// Range of a tensor (round 6, dcx_kernels.h h2_shift): in the h2 layout it holds x * 2^ash[clip]
+// (ash null: ash_c for every clip); |x| <= max(amax[clip], amax_f) (amax null: amax_f), the input
+// term of its consumers' bound programs.
+// ash_row (one-tap consumers): a shift per row instead.
+struct Rng {
+  const int* ash = nullptr;
+  int ash_c = 0;
+  const float* amax = nullptr;
+  float amax_f = 0.f;
+  const int* ash_row = nullptr;
+};
 struct Act {
   float* f = nullptr;
   unsigned short* p = nullptr;
   bool c1 = false;
   bool h2 = false;
+  Rng r;
+  // per-row range buffers an h2 producer fills for a one-tap consumer (round 6): the shift and (for
+  // LayerNorm outputs) the max |.| of each row
+  int* row_ash = nullptr;
+  float* row_amax = nullptr;
 };
 struct CAct {
   const float* f = nullptr;
   const unsigned short* p = nullptr;
   bool c1 = false;
   bool h2 = false;
+  Rng r;
   CAct() = default;
   CAct(const float* f_, const unsigned short* p_, bool c1_ = false) : f(f_), p(p_), c1(c1_) {}
-  CAct(const Act& a) : f(a.f), p(a.p), c1(a.c1), h2(a.h2) {}
+  CAct(const Act& a) : f(a.f), p(a.p), c1(a.c1), h2(a.h2), r(a.r) {}
 };
+// bound programs (dcx::RangeProg): c + sum of g * max(measured, floor) terms
+void prog_add(dcx::RangeProg& p, float g, const Rng& r) {
+  p.m[p.n] = r.amax;
+  p.g[p.n] = g;
+  p.f[p.n] = r.amax_f;
+  ++p.n;
+}
+// |conv(x) + bias| <= g_abs max|x| + b_abs (|silu(v)|, |gelu(v)| <= |v|)
+dcx::RangeProg prog_conv(const ConvW& w, const Rng& in) {
+  dcx::RangeProg p{};
+  p.c = w.b_abs;
+  prog_add(p, w.g_abs, in);
+  return p;
+}
+// per-row bound of a one-tap conv's output from its input rows' maxima (rowwise program)
+dcx::RangeProg prog_conv_rows(const ConvW& w, const float* in_row_amax) {
+  dcx::RangeProg p{};
+  p.rowwise = 1;
+  p.c = w.b_abs;
+  p.m[0] = in_row_amax;
+  p.g[0] = w.g_abs;
+  p.n = 1;
+  return p;
+}
 
 // planes layout for every GEMM operand (x6 and bf16 modes)
 bool x6_mode(const dcx_codec* h) { return h->gemm_mode != DCX_GEMM_F32; }
@@ -619,12 +690,33 @@ struct ConvCall {
   int epi = dcx::EPI_BIAS, mean = dcx::MEAN_NONE;
   bool exact = false;  // keep x6 arithmetic in bf16 mode (the reference's fp32 mel front end)
   bool silu_in = false;  // fp32 input: the conv consumes silu(x) (applied while staging)
+  // h3 range (round 6): the bound program of an h2 output, where its per-clip shift goes, and where
+  // the per-clip max |v| of the output goes (ConvParams::yb / y_ash / y_amax)
+  dcx::RangeProg yb{};
+  int* y_ash = nullptr;
+  float* y_amax = nullptr;
   void silu_to(const Act& a) {
     y2 = a.f;
     y6s = a.p;
     y6s_h2 = a.h2;
   }
   void out_to(const Act& a) { y = a.f; y6 = a.p; y6c = a.c1 ? 1 : a.h2 ? 3 : 0; }
+};
+
+// Per-call range slots of the generator (round 6): measured per-clip maxima and h2 shifts, [slot][clip],
+// zeroed once at the start of the call (one memset; capture-safe).
+struct RangeArena {
+  float* base = nullptr;
+  int batch = 0, used = 0;
+  static constexpr int kSlots = 320;
+  void reserve(Bump& ws, int b) {
+    batch = b;
+    base = ws.f((size_t)kSlots * b);
+  }
+  // h3 range slots are only consumed by h2 tensors; a call past the capacity fails loudly
+  float* amax() { return used < kSlots && base ? base + (size_t)(used++) * batch : nullptr; }
+  int* ash() { return reinterpret_cast<int*>(amax()); }
+  bool ok() const { return used < kSlots; }
 };
 
 // Planes-mode convs with Cout <= 64, Cin <= 128 and a tap halo take an fp32 input (split while
@@ -710,7 +802,16 @@ int conv_params(dcx_codec* h, const ConvW& w, const ConvCall& c, bool force_f32,
     p.x_compact = 3;
     p.w3 = w.w3;
     p.w3_shift = w.w3_shift;
+    p.x_ash = c.x.r.ash;
+    p.x_ash_c = c.x.r.ash_c;
+    p.x_ash_row = c.x.r.ash_row;
+    if (p.x_ash_row && (w.taps != 1 || w.phases != 1 || w.in_base[0] != 0))
+      return fail(h, DCX_ERR_STATE, "internal: per-row input ranges need a one-tap conv");
   }
+  p.y_ash = c.y_ash;
+  p.y_amax = c.y_amax;
+  p.yb = c.yb;
+  p.rflag = h->rflag;
   p.wc = one && h->compact ? w.wc : nullptr;
   p.kn = &h->knobs;
   // compact inputs only feed one-product GEMMs; a compact output (the RNE hi value) may also be written
@@ -731,8 +832,15 @@ bool takes_compact(const dcx_codec* h, const ConvW& w, long long rows) {
 // Whether a generator conv with a tap halo (conv_pre, the ConvTs with Cout % 128 == 0) runs in h3
 // arithmetic (conv_gemm_x3dw; Knobs::h3, x6 mode, not in the split-K latency mode), so its producer
 // writes h2.
-bool takes_h3_conv(const dcx_codec* h, const ConvW& w) {
-  return h->knobs.h3 && h->gemm_mode == DCX_GEMM_X6 && h->split_k < 2 && w.w3 && w.taps >= 2 && w.cout % 128 == 0;
+// The h3 tap kernels address a clip's input through one buffer descriptor: (rows + 1024) * Cin * 4
+// bytes must stay under 2^31 (dcx_conv.hip x3dq_ok); longer clips (> ~11 min at the C = 256 stage)
+// keep the x6 kernels, whose tiles rebase their descriptors.
+bool h3_rows_ok(long long rows, int cin) { return (rows + 1024) * cin * 4LL < (1LL << 31); }
+
+// rows: the conv's input rows per clip
+bool takes_h3_conv(const dcx_codec* h, const ConvW& w, long long rows) {
+  return h->knobs.h3 && h->gemm_mode == DCX_GEMM_X6 && h->split_k < 2 && w.w3 && w.taps >= 2 && w.cout % 128 == 0 &&
+         h3_rows_ok(rows, w.cin);
 }
 
 // Whether a one-tap conv runs in h3 arithmetic (conv_gemm_x3dm; Knobs::h3_1x1, x6 mode, not in the
@@ -791,6 +899,8 @@ int run_conv_split(dcx_codec* h, const ConvW& w, const ConvCall& c, const ConvPa
   q.mean_mode = dcx::MEAN_NONE;
   q.y_compact = 0;
   q.round_bf16 = 0;
+  q.y_ash = nullptr;  // the slices' clips are virtual; the split-K mode runs no h3 conv
+  q.y_amax = nullptr;
   const char* kname = "conv";
   HIPCHK(h, dcx::launch_conv(q, c.batch * S, w.phases, s, &kname));
   HIPCHK(h, dcx::launch_splitk_epilogue(p, h->split_buf, S, (long long)c.batch * p.y_bstride, c.batch, w.phases, s));
@@ -900,6 +1010,8 @@ int run_conv_group_split(dcx_codec* h, const ConvW* const* w, const ConvCall* c,
       q[i].mean_mode = dcx::MEAN_NONE;
       q[i].y_compact = 0;
       q[i].round_bf16 = 0;
+      q[i].y_ash = nullptr;  // virtual clips (run_conv_split)
+      q[i].y_amax = nullptr;
       r[nr] = p[i];
       part[nr] = h->split_buf + off;
       rs[nr] = S[i];
@@ -989,44 +1101,78 @@ ConvCall framed(CAct x, int B, int L, int C) {
   } while (0)
 
 // fp32 -> planes (or, with compact, bf16) for a tensor handed in by the caller (x6 / bf16 modes).
-// h2: the h2 layout instead (an h3 consumer; a planes tensor handed in with its fp32 copy is re-split)
+// h2: the h2 layout instead (an h3 consumer; a planes tensor handed in with its fp32 copy is re-split),
+// range-scaled (dcx_kernels.h h2_shift) by the exact max of each clip (`clips` clips of rows / clips
+// rows: launch_h2_ranged, for the tap convs) or, with clips == 0, of each row (launch_h2_rows, for the
+// one-tap convs).  The scale follows from the values alone, so a tensor the fused pipeline would have
+// produced in h2 itself (a LayerNorm's row-scaled output) gets the same bits here.
 int ensure_planes(dcx_codec* h, CAct& a, long long rows, int C, Bump& ws, hipStream_t s, bool compact = false,
-                  bool h2 = false) {
+                  bool h2 = false, int clips = 0) {
   if (h2 && a.p && !a.h2 && a.f) a.p = nullptr;
   if (!x6_mode(h) || a.p) return DCX_OK;
+  const bool rh2 = h2 && !compact;
   unsigned short* p = ws.u16((size_t)rows * C * 3);
+  float* am = rh2 && clips ? ws.f((size_t)clips) : nullptr;
+  int* ash = rh2 ? ws.i((size_t)(clips ? clips : rows)) : nullptr;
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small");
-  LAUNCH(h, s, "split_planes", 0, (compact ? 6.0 : h2 ? 8.0 : 10.0) * rows * C,
-         dcx::launch_split_planes(a.f, p, rows, C, compact ? 1 : h2 ? 3 : 0, s));
+  if (rh2 && clips) {
+    if (clips < 1 || rows % clips) return fail(h, DCX_ERR_STATE, "internal: ranged split of a ragged batch");
+    LAUNCH(h, s, "h2_ranged", 0, 12.0 * rows * C,
+           dcx::launch_h2_ranged(a.f, nullptr, p, clips, rows / clips, C, 0, 0.f, am, ash, h->rflag, s));
+    a.r = Rng{};
+    a.r.ash = ash;
+    a.r.amax = am;
+  } else if (rh2) {
+    LAUNCH(h, s, "h2_rows", 0, 8.0 * rows * C, dcx::launch_h2_rows(a.f, p, rows, C, ash, s));
+    a.r = Rng{};
+    a.r.ash_row = ash;
+  } else {
+    LAUNCH(h, s, "split_planes", 0, (compact ? 6.0 : 10.0) * rows * C,
+           dcx::launch_split_planes(a.f, p, rows, C, compact ? 1 : 0, s));
+  }
   a.p = p;
   a.c1 = compact;
-  a.h2 = h2 && !compact;
+  a.h2 = rh2;
   return DCX_OK;
 }
 
 // ConvNeXtBlock in place on x [B][T][C] (fp32 residual stream); out6: optional planes (compact
 // with out6c) of the block output for a following conv.  ln: [M][C], hid: [M][4C] conv-input
 // scratch, written compact where their consumer takes it (bf16 mode).
+// ConvNeXtBlock in place on x [B][T][C] (fp32 residual stream); out6: optional planes (compact
+// with out6c = 1) of the block output for a following conv.  ln: [M][C], hid: [M][4C] conv-input
+// scratch, written compact where their consumer takes it (bf16 mode), or in h2 with per-row ranges
+// (ln.row_ash / row_amax, hid.row_ash: the LayerNorm's exact row maxima, the hidden's rows bounded
+// by g1 max|LN row| + max|b1|; round 6).
 int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, int B, int T, Act ln, Act hid,
               hipStream_t s, int out6c = 0) {
   const long long M = (long long)B * T;
   const int C = bw.C;
+  if (out6 && out6c == 3) return fail(h, DCX_ERR_STATE, "internal: a block output in h2 goes through launch_h2_rows");
   ln.c1 = ln.p && takes_compact(h, bw.pw1, M);
   hid.c1 = hid.p && takes_compact(h, bw.pw2, M);
-  ln.h2 = ln.p && takes_h3(h, bw.pw1);
-  hid.h2 = hid.p && takes_h3(h, bw.pw2);
+  ln.h2 = ln.p && ln.row_ash && ln.row_amax && takes_h3(h, bw.pw1);
+  hid.h2 = hid.p && hid.row_ash && takes_h3(h, bw.pw2);
+  ln.r = Rng{};
+  hid.r = Rng{};
+  ln.r.ash_row = ln.row_ash;
+  hid.r.ash_row = hid.row_ash;
   LAUNCH(h, s, "dwconv_ln", 14.0 * M * C, 8.0 * M * C,
          dcx::launch_dwconv_ln(x, ln.f, ln.p, ln.c1 ? 1 : ln.h2 ? 3 : 0, bw.dww, bw.dwb, bw.ln.w, bw.ln.b, B, T, C,
-                               h->gemm_mode == DCX_GEMM_BF16 ? 1 : 0, &h->knobs, s));
+                               h->gemm_mode == DCX_GEMM_BF16 ? 1 : 0, &h->knobs, s, ln.row_ash, ln.row_amax));
   ConvCall c1 = pointwise(ln, M);
   c1.out_to(hid);
   c1.epi = dcx::EPI_GELU;
+  if (hid.h2) {  // |GELU(v)| <= |v| <= g1 max|LN row| + max|b1|
+    c1.yb = prog_conv_rows(bw.pw1, ln.row_amax);
+    c1.y_ash = hid.row_ash;
+  }
   RUN(run_conv(h, bw.pw1, c1, s));
   ConvCall c2 = pointwise(hid, M);
   c2.y = x;
   c2.y6 = out6;
-  c2.y6c = out6 ? out6c : 0;  // 0 planes, 1 compact, 3 h2
+  c2.y6c = out6 ? out6c : 0;  // 0 planes, 1 compact
   c2.res = x;
   c2.gamma = bw.gamma;
   c2.epi = dcx::EPI_GAMMA_RES;
@@ -1035,12 +1181,23 @@ int run_block(dcx_codec* h, const BlockW& bw, float* x, unsigned short* out6, in
 }
 
 // channels-first LayerNorm; bf16_in: its input is a bf16 tensor under the reference's autocast (the
-// stem's, in bf16 mode), so its mean and differences are bf16 (ln_rows form 2)
+// stem's, in bf16 mode), so its mean and differences are bf16 (ln_rows form 2).  An h2 output (y.h2)
+// is scaled per row by its exact max (y.row_ash receives the shifts, y.row_amax the maxima if set).
 int run_ln(dcx_codec* h, const LnW& l, const float* x, Act y, long long rows, hipStream_t s, bool bf16_in = false) {
   const int form = bf16_in && h->gemm_mode == DCX_GEMM_BF16 ? 2 : 1;
+  if (y.p && y.h2 && !y.row_ash) return fail(h, DCX_ERR_STATE, "internal: h2 LayerNorm output without row ranges");
   LAUNCH(h, s, "ln_rows", 8.0 * rows * l.C, 8.0 * rows * l.C,
-         dcx::launch_ln_rows(x, y.f, y.p, y.p && y.c1 ? 1 : y.p && y.h2 ? 3 : 0, l.w, l.b, rows, l.C, 1e-6f, form, s));
+         dcx::launch_ln_rows(x, y.f, y.p, y.p && y.c1 ? 1 : y.p && y.h2 ? 3 : 0, l.w, l.b, rows, l.C, 1e-6f, form, s,
+                             y.row_ash, y.row_amax));
   return DCX_OK;
+}
+
+// Per-row range buffers for the block scratch of M rows (x6 mode only: the h3 one-tap convs).
+void row_ranges(dcx_codec* h, Bump& ws, long long M, Act& ln, Act& hid) {
+  if (!x6_mode(h)) return;
+  ln.row_ash = ws.i((size_t)M);
+  ln.row_amax = ws.f((size_t)M);
+  hid.row_ash = ws.i((size_t)M);
 }
 
 // ---------------- stage bodies (dry=true only sizes the workspace) ----------------
@@ -1081,6 +1238,7 @@ int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipSt
   float* xb = ws.f((size_t)M * cmax);
   Act ln = conv_input(h, ws, (size_t)M * cmax);
   Act hid = conv_input(h, ws, (size_t)M * 4 * cmax);
+  row_ranges(h, ws, M, ln, hid);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for encode");
   ConvCall cc = framed(mel, B, T, c.n_mels);
@@ -1090,7 +1248,9 @@ int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipSt
   for (int i = 0; i < 4; ++i) {
     if (i > 0) {
       ln.c1 = ln.p && takes_compact(h, h->ds_conv[i], M);
-      ln.h2 = ln.p && takes_h3(h, h->ds_conv[i]);  // the downsample 1x1 conv on conv_gemm_x3dw
+      ln.h2 = ln.p && ln.row_ash && takes_h3(h, h->ds_conv[i]);  // the downsample 1x1 conv on conv_gemm_x3dw
+      ln.r = Rng{};
+      ln.r.ash_row = ln.h2 ? ln.row_ash : nullptr;  // row-scaled by run_ln
       RUN(run_ln(h, h->ds_ln[i], xb, ln, M, s));
       ConvCall cd = pointwise(ln, M);
       cd.y = xb;
@@ -1098,7 +1258,7 @@ int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipSt
     }
     for (auto& bw : h->blocks[i]) RUN(run_block(h, bw, xb, nullptr, B, T, ln, hid, s));
   }
-  RUN(run_ln(h, h->enc_norm, xb, feat, M, s));
+  RUN(run_ln(h, h->enc_norm, xb, feat, M, s));  // an h2 feat: row-scaled into feat.row_ash
   return DCX_OK;
 }
 
@@ -1213,12 +1373,20 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   const bool x6 = x6_mode(h);
   const int xl = vq_xlayout(h, M);
   const int ntiles = x6 ? dcx::vq_prefilter_ntiles(NC, CD, M, xl) : dcx::vq_argmin_ntiles(NC);
-  RUN(ensure_planes(h, feat, M, D, ws, s, takes_compact(h, h->vq_down, M)));
+  // the down conv's input as the fused pipeline writes it: compact bf16 (bf16 mode) or h2 (h3), the
+  // latter scaled per row by the row's exact max as the encoder's final LayerNorm scales it, so the
+  // staged and the fused call compute the same bits
+  {
+    const bool cmp = takes_compact(h, h->vq_down, M);
+    RUN(ensure_planes(h, feat, M, D, ws, s, cmp, !cmp && takes_h3(h, h->vq_down), 0));
+  }
   if (feat.c1 && !takes_compact(h, h->vq_down, M)) return fail(h, DCX_ERR_STATE, "internal: compact features");
   float* X = ws.f((size_t)M * D);
   unsigned short* X6 = x6 ? ws.u16((size_t)M * D * 3) : nullptr;
   Act ln = conv_input(h, ws, (size_t)M * D);
   Act hid = conv_input(h, ws, (size_t)M * 4 * D);
+  row_ranges(h, ws, M, ln, hid);
+  int* x6_ash = x6 ? ws.i((size_t)M) : nullptr;  // project_in's input rows' shifts (h3)
   float* P = pin ? pin : ws.f((size_t)M * CD);
   unsigned short* P6 = x6 ? ws.u16((size_t)M * CD * 3) : nullptr;
   const VqScratch vs = vq_scratch(h, ws, M, ntiles, x6);
@@ -1230,9 +1398,13 @@ int stage_vq_encode(dcx_codec* h, CAct feat, int B, int T, int32_t* codes, float
   RUN(run_conv(h, h->vq_down, cd, s));
   const bool x6c = X6 && takes_compact(h, h->vq_pin, M);
   const bool h2p = X6 && !x6c && takes_h3(h, h->vq_pin);  // project_in on conv_gemm_x3dw
-  RUN(run_block(h, h->vq_down_blk, X, X6, B, T, ln, hid, s, x6c ? 1 : h2p ? 3 : 0));
+  // the block's output for project_in: compact / planes from its epilogue, or (h3) split per row by
+  // the row's exact max afterwards (launch_h2_rows)
+  RUN(run_block(h, h->vq_down_blk, X, h2p ? nullptr : X6, B, T, ln, hid, s, x6c ? 1 : 0));
+  if (h2p) LAUNCH(h, s, "h2_rows", 0, 8.0 * M * D, dcx::launch_h2_rows(X, X6, M, D, x6_ash, s));
   CAct pin_in(X, X6, x6c);
   pin_in.h2 = h2p;
+  if (h2p) pin_in.r.ash_row = x6_ash;
   ConvCall cp = pointwise(pin_in, M);
   cp.y = P;
   cp.y6 = P6;
@@ -1263,8 +1435,10 @@ int stage_vq_decode(dcx_codec* h, const int32_t* codes, int B, int T, Act z, int
   Act zd = conv_input(h, ws, (size_t)M * D);
   Act ln = conv_input(h, ws, (size_t)M * D);
   Act hid = conv_input(h, ws, (size_t)M * 4 * D);
+  row_ranges(h, ws, M, ln, hid);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for vq_decode");
+  if (z.p && z.h2) return fail(h, DCX_ERR_STATE, "internal: z in h2 is split by the generator (ranged per clip)");
   if (x6_mode(h))
     LAUNCH(h, s, "gather_rows", 0, 12.0 * M * D,
            dcx::launch_gather_rows((const float*)decode_table6(h), c.codebook_size, codes, M, D * 3 / 2, (float*)zd.p,
@@ -1275,7 +1449,7 @@ int stage_vq_decode(dcx_codec* h, const int32_t* codes, int B, int T, Act z, int
   ConvCall cu = pointwise(zd, M);
   cu.y = z.f;
   RUN(run_conv(h, h->vq_up, cu, s));
-  RUN(run_block(h, h->vq_up_blk, z.f, z.p, B, T, ln, hid, s, z.h2 ? 3 : 0));
+  RUN(run_block(h, h->vq_up_blk, z.f, z.p, B, T, ln, hid, s));
   return DCX_OK;
 }
 
@@ -1300,8 +1474,10 @@ bool res_pair_ok(const dcx_codec* h, int stage) {
 // Whether generator stage i runs its ResBlock convs in h3 arithmetic (Knobs::h3, x6 mode, not in
 // the split-K latency mode, every conv with h3 weights): their inputs are then written in the h2
 // layout by their producers (ConvT, c1, c2 epilogues).
-bool h3_stage(const dcx_codec* h, int i) {
+// rows: the stage's rows per clip (its ResBlock convs' input length)
+bool h3_stage(const dcx_codec* h, int i, long long rows) {
   if (!h->knobs.h3 || h->gemm_mode != DCX_GEMM_X6 || h->split_k >= 2) return false;
+  if (!h3_rows_ok(rows, h->res[i][0][0][0].cin)) return false;
   for (int rb = 0; rb < h->cfg.n_res; ++rb)
     for (int j = 0; j < 3; ++j)
       if (!h->res[i][rb][j][0].w3 || !h->res[i][rb][j][1].w3) return false;
@@ -1319,18 +1495,26 @@ struct PBlockBufs {
   float* Mx = nullptr;               // mean accumulator; silu(mean) in fp32 when `last`
   Act next;                          // silu(mean) in the next ConvT's input form (not `last`)
   bool last = false;
+  // h3 ranges (round 6): the measured per-clip max |X| (XS.r carries its h2 shift), the slots that
+  // receive the mean's max |.| and h2 shift (not `last`), and the call's slots for everything else
+  const float* amax_X = nullptr;
+  float* next_amax = nullptr;
+  int* next_ash = nullptr;
+  RangeArena* ra = nullptr;
 };
 
 // ParralelBlock.forward (convnext_utils.py:137-138) of generator stage i: three ResBlock1
 // (convnext_utils.py:106-113) on X, their mean, and the SiLU that follows it in the generator
 // (generators.py:125 / :141), written to b.Mx as fp32 (b.last) or to b.next.  The C = 32 / 64
-// stages run as fused pairs (conv_res_pair), the others as grouped per-conv launches.
+// stages run as fused pairs (conv_res_pair), the others as grouped per-conv launches.  Every h2
+// tensor is range-scaled from a bound over the maxima its producers measured (dcx_kernels.h).
 int run_parallel_block(dcx_codec* h, int i, int B, int Lo, const PBlockBufs& b, hipStream_t s) {
   const dcx_config& c = h->cfg;
   constexpr int NR = dcx::kMaxGroup;
   const ConvW& rconv = h->res[i][0][0][0];  // every ResBlock conv of the stage has Cin = Cout = Co
   const int Co = rconv.cout;
   const bool silu_on_load = x6_mode(h) && f32_input_ok(rconv);
+  RangeArena& ra = *b.ra;
   if (silu_on_load && res_pair_ok(h, i)) {
     // fused pairs: X -> R[rb] -> Tb[rb] (as fp32) -> silu(ParallelBlock mean)
     float* Ra[NR];
@@ -1343,6 +1527,8 @@ int run_parallel_block(dcx_codec* h, int i, int B, int Lo, const PBlockBufs& b, 
     bool h3 = h->knobs.h3_pairs && h->split_k < 2;  // conv_res_pair_h3 (every conv with h3 weights)
     for (int rb = 0; rb < c.n_res; ++rb)
       for (int ci = 0; ci < 3; ++ci) h3 = h3 && h->res[i][rb][ci][0].w3 && h->res[i][rb][ci][1].w3;
+    const float* st_amax[NR];  // measured max |state| per clip of each ResBlock's pair input
+    for (int rb = 0; rb < c.n_res; ++rb) st_amax[rb] = b.amax_X;
     for (int ci = 0; ci < 3; ++ci) {
       dcx::ResPairParams rp{};
       rp.h3 = h3 ? 1 : 0;
@@ -1360,6 +1546,10 @@ int run_parallel_block(dcx_codec* h, int i, int B, int Lo, const PBlockBufs& b, 
         rp.b2[rb] = w2.b;
         rp.taps[rb] = w1.taps;
         rp.dil[rb] = w1.in_step;
+        rp.src_amax[rb] = st_amax[rb];
+        rp.dst_amax[rb] = ci < 2 ? ra.amax() : nullptr;
+        rp.g1[rb] = w1.g_abs;
+        rp.bm1[rb] = w1.b_abs;
         ConvCall cc = framed(Act{b.X, nullptr}, B, Lo, Co);
         fl += conv_flops(w1, cc) + conv_flops(w2, cc);
         by += 8.0 * B * Lo * Co;
@@ -1370,53 +1560,99 @@ int run_parallel_block(dcx_codec* h, int i, int B, int Lo, const PBlockBufs& b, 
       rp.L = Lo;
       rp.batch = B;
       rp.C = Co;
+      rp.rflag = h->rflag;
       rp.kn = &h->knobs;
+      if (h3)
+        for (int rb = 0; rb < c.n_res; ++rb)
+          if (!rp.src_amax[rb] || (ci < 2 && !rp.dst_amax[rb]))
+            return fail(h, DCX_ERR_STATE, "internal: h3 range slots exhausted");
       ProfScope ps(h, s);
       const char* kname = "conv_res_pair";
       HIPCHK(h, dcx::launch_res_pair(rp, s, &kname));
       ps.done(kname, fl, by);
+      for (int rb = 0; rb < c.n_res; ++rb) st_amax[rb] = rp.dst_amax[rb];
     }
     return DCX_OK;
+  }
+  // ranges of each ResBlock's state (its max |.|) and of the c1 inputs in h2
+  Rng st[NR], in1[NR];
+  for (int rb = 0; rb < c.n_res; ++rb) {
+    st[rb].amax = b.amax_X;
+    in1[rb] = b.XS.r;
+    in1[rb].amax = b.amax_X;
   }
   for (int ci = 0; ci < 3; ++ci) {
     const ConvW* w1[NR];
     ConvCall c1[NR];
+    Rng tr[NR];  // silu(c1 output): shift and the measured max |c1 output|
     for (int rb = 0; rb < c.n_res; ++rb) {  // c1 of every ResBlock: one grouped launch
-      const Act src = silu_on_load ? Act{ci == 0 ? b.X : b.R[rb], nullptr} : (ci == 0 ? b.XS : b.RS[rb]);
+      Act src = silu_on_load ? Act{ci == 0 ? b.X : b.R[rb], nullptr} : (ci == 0 ? b.XS : b.RS[rb]);
+      src.r = in1[rb];
       c1[rb] = framed(src, B, Lo, Co);
       c1[rb].silu_in = silu_on_load;
       c1[rb].silu_to(b.Tb_in[rb]);
       w1[rb] = &h->res[i][rb][ci][0];
+      c1[rb].yb = prog_conv(*w1[rb], in1[rb]);
+      c1[rb].y_amax = ra.amax();
+      c1[rb].y_ash = b.Tb_in[rb].h2 ? ra.ash() : nullptr;
+      tr[rb].ash = c1[rb].y_ash;
+      tr[rb].amax = c1[rb].y_amax;
     }
     RUN(run_conv_group(h, w1, c1, c.n_res, s));
     if (ci < 2) {  // c2 of every ResBlock: grouped; residual X (first pair) or the block's state
       const ConvW* w2[NR];
       ConvCall c2[NR];
       for (int rb = 0; rb < c.n_res; ++rb) {
-        c2[rb] = framed(b.Tb_in[rb], B, Lo, Co);
+        Act tin = b.Tb_in[rb];
+        tin.r = tr[rb];
+        c2[rb] = framed(tin, B, Lo, Co);
         c2[rb].epi = dcx::EPI_RES;
         c2[rb].res = ci == 0 ? b.X : b.R[rb];
         c2[rb].y = b.R[rb];
         if (!silu_on_load) c2[rb].silu_to(b.RS[rb]);
         w2[rb] = &h->res[i][rb][ci][1];
+        // |state + c2 + b2| <= max|state| + g2 max|c1 output| + max|b2|
+        c2[rb].yb.c = w2[rb]->b_abs;
+        prog_add(c2[rb].yb, 1.0f, st[rb]);
+        prog_add(c2[rb].yb, w2[rb]->g_abs, tr[rb]);
+        c2[rb].y_amax = ra.amax();
+        c2[rb].y_ash = !silu_on_load && b.RS[rb].h2 ? ra.ash() : nullptr;
       }
       RUN(run_conv_group(h, w2, c2, c.n_res, s));
+      for (int rb = 0; rb < c.n_res; ++rb) {
+        st[rb] = Rng{};
+        st[rb].amax = c2[rb].y_amax;
+        in1[rb] = Rng{c2[rb].y_ash, 0, c2[rb].y_amax, 0.f};
+      }
     } else {  // last pair: ParallelBlock mean folded into the epilogues, in ResBlock order
       const ConvW* w2[NR];
       ConvCall cm[NR];
       for (int rb = 0; rb < c.n_res; ++rb) {
         ConvCall& cc = cm[rb];
-        cc = framed(b.Tb_in[rb], B, Lo, Co);
+        Act tin = b.Tb_in[rb];
+        tin.r = tr[rb];
+        cc = framed(tin, B, Lo, Co);
         cc.epi = dcx::EPI_RES;
         cc.res = b.R[rb];
         cc.macc = b.Mx;
         cc.mean = rb == 0 ? dcx::MEAN_FIRST : (rb == c.n_res - 1 ? dcx::MEAN_LAST : dcx::MEAN_MID);
+        w2[rb] = &h->res[i][rb][ci][1];
         if (rb == c.n_res - 1) {
           // silu(mean): input of ups[i+1], or (fp32, in place) of conv_post
           if (b.last) cc.y2 = b.Mx;
           else cc.silu_to(b.next);  // input of the next ConvT
+          // |mean| <= (1/3) sum over the ResBlocks of (max|state| + g2 max|c1 output| + max|b2|)
+          float bc = 0.f;
+          for (int m = 0; m < c.n_res; ++m) {
+            const ConvW& wm = h->res[i][m][ci][1];
+            bc += wm.b_abs / 3.0f;
+            prog_add(cc.yb, 1.0f / 3.0f, st[m]);
+            prog_add(cc.yb, wm.g_abs / 3.0f, tr[m]);
+          }
+          cc.yb.c = Builder::round_up((double)bc * (1.0 + 1e-6));
+          cc.y_amax = b.next_amax;
+          cc.y_ash = b.next_ash;
         }
-        w2[rb] = &h->res[i][rb][ci][1];
       }
       // split-K mode: one grouped launch and one chained reduce; otherwise conv by conv (the
       // mean's order forbids the grouped unsplit kernel)
@@ -1436,17 +1672,28 @@ int run_parallel_block(dcx_codec* h, int i, int B, int Lo, const PBlockBufs& b, 
         for (int rb = 0; rb < c.n_res; ++rb) RUN(run_conv(h, *w2[rb], cm[rb], s));
     }
   }
+  if (!ra.ok()) return fail(h, DCX_ERR_STATE, "internal: h3 range slots exhausted");
   return DCX_OK;
+}
+
+// a tensor consumed by a small-Cout conv in fp32 (those kernels split while staging), range kept
+Act fp32_form(dcx_codec* h, const Act& a, const ConvW& consumer) {
+  if (!x6_mode(h) || !f32_input_ok(consumer)) return a;
+  Act f{a.f ? a.f : reinterpret_cast<float*>(a.p), nullptr};
+  f.r = a.r;
+  return f;
 }
 
 int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hipStream_t s) {
   const dcx_config& c = h->cfg;
-  RUN(ensure_planes(h, z, (long long)B * T, c.vq_dim, ws, s, false, takes_h3_conv(h, h->conv_pre)));
+  // z in conv_pre's h2 form, range-scaled by each clip's exact max (the fused pipeline's z as well)
+  RUN(ensure_planes(h, z, (long long)B * T, c.vq_dim, ws, s, false, takes_h3_conv(h, h->conv_pre, T), B));
   const size_t per = (size_t)B * T * max_gen_width(c);
   // The ParallelBlock's ResBlocks are independent until the mean, so each keeps its own state and
   // the convs of one dilation index run as one grouped launch (run_conv_group).
   constexpr int NR = dcx::kMaxGroup;
   if (c.n_res > NR) return fail(h, DCX_ERR_INVALID_ARG, "more ResBlocks per stage than supported");
+  if (2 + 36 * c.n_ups > RangeArena::kSlots) return fail(h, DCX_ERR_INVALID_ARG, "too many generator stages");
   float* X = ws.f(per);   // ConvT output (residual of each ResBlock's first pair)
   float* Mx = ws.f(per);  // ParallelBlock mean accumulator; silu(mean) of the last stage
   Act S = conv_input(h, ws, per);   // silu(stage input) -> ConvT
@@ -1458,28 +1705,32 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
     RS[rb] = conv_input(h, ws, per);
     Tb[rb] = conv_input(h, ws, per);
   }
+  RangeArena ra;
+  ra.reserve(ws, B);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for generate");
+  HIPCHK(h, dcx::launch_zero_words(ra.base, (long long)RangeArena::kSlots * B, s));
   // Tensors consumed by small-Cout convs are kept in fp32 (those kernels split them while
   // staging: the stages are bound by HBM traffic, and planes cost 6 B per element against 4).
-  auto in_form = [&](const Act& a, const ConvW& consumer) -> Act {
-    if (!x6_mode(h) || !f32_input_ok(consumer)) return a;
-    return Act{a.f ? a.f : reinterpret_cast<float*>(a.p), nullptr};
-  };
+  auto in_form = [&](const Act& a, const ConvW& consumer) -> Act { return fp32_form(h, a, consumer); };
   int C = c.gen_channels, L = T;
   {  // conv_pre, then the first stage's SiLU (generators.py:121,125) fused as the only output
     ConvCall cc = framed(z, B, T, c.vq_dim);
     Act S0 = S;
-    S0.h2 = S.p && takes_h3_conv(h, h->ups[0]);
+    S0.h2 = S.p && takes_h3_conv(h, h->ups[0], T);
     cc.silu_to(S0);
+    cc.yb = prog_conv(h->conv_pre, z.r);
+    cc.y_amax = ra.amax();
+    cc.y_ash = S0.h2 ? ra.ash() : nullptr;
     RUN(run_conv(h, h->conv_pre, cc, s));
+    S.r = Rng{cc.y_ash, 0, cc.y_amax, 0.f};
   }
   for (int i = 0; i < c.n_ups; ++i) {
     const ConvW& up = h->ups[i];
     const int Co = up.cout, Lo = L * c.up_rates[i];
     const ConvW& rconv = h->res[i][0][0][0];  // every ResBlock conv of the stage has Cin = Cout = Co
     Act S_i = in_form(S, up);
-    S_i.h2 = S_i.p && takes_h3_conv(h, up);  // as conv_pre / the previous stage's mean epilogue wrote it
+    S_i.h2 = S_i.p && takes_h3_conv(h, up, L);  // as conv_pre / the previous stage's mean epilogue wrote it
     Act XS_i = in_form(XS, rconv);
     Act RS_i[NR], Tb_i[NR];
     for (int rb = 0; rb < c.n_res; ++rb) {
@@ -1489,15 +1740,20 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
     // fp32-input stages: the first conv of each pair applies silu to X / R while staging, so
     // silu(X) and silu(R) are never written (7 activation tensors per stage less HBM traffic)
     const bool silu_on_load = x6_mode(h) && f32_input_ok(rconv);
-    if (h3_stage(h, i)) {  // the ResBlock convs' inputs in the h2 layout (conv_gemm_x3dq)
+    if (h3_stage(h, i, Lo)) {  // the ResBlock convs' inputs in the h2 layout (conv_gemm_x3dq)
       XS_i.h2 = true;
       for (int rb = 0; rb < c.n_res; ++rb) RS_i[rb].h2 = Tb_i[rb].h2 = true;
     }
+    float* amax_X = ra.amax();
     {
       ConvCall cc = framed(S_i, B, L, C);
       cc.y = X;
       if (!silu_on_load) cc.silu_to(XS_i);
+      cc.yb = prog_conv(up, S_i.r);
+      cc.y_amax = amax_X;
+      cc.y_ash = !silu_on_load && XS_i.h2 ? ra.ash() : nullptr;
       RUN(run_conv(h, up, cc, s));
+      XS_i.r = Rng{cc.y_ash, 0, amax_X, 0.f};
     }
     PBlockBufs pb;
     pb.X = X;
@@ -1510,11 +1766,17 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
     }
     pb.Mx = Mx;
     pb.last = i == c.n_ups - 1;
+    pb.amax_X = amax_X;
+    pb.ra = &ra;
     if (!pb.last) {
       pb.next = in_form(S, h->ups[i + 1]);
-      pb.next.h2 = pb.next.p && takes_h3_conv(h, h->ups[i + 1]);
+      pb.next.h2 = pb.next.p && takes_h3_conv(h, h->ups[i + 1], Lo);
+      pb.next_amax = ra.amax();
+      pb.next_ash = pb.next.h2 ? ra.ash() : nullptr;
     }
+    if (!ra.ok()) return fail(h, DCX_ERR_STATE, "internal: h3 range slots exhausted");
     RUN(run_parallel_block(h, i, B, Lo, pb, s));
+    S.r = Rng{pb.next_ash, 0, pb.next_amax, 0.f};
     C = Co;
     L = Lo;
   }
@@ -1534,10 +1796,14 @@ int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int3
   Act feat = conv_input(h, ws, (size_t)M * c.enc_dims[3]);
   feat.c1 = feat.p && takes_compact(h, h->vq_down, M);  // written by the encoder's final LayerNorm
   feat.h2 = feat.p && !feat.c1 && takes_h3(h, h->vq_down);  // h2 for the quantizer's down conv (x3dw)
+  // (reserved whenever x6 mode could write it: a dry run sees no pointers, so sizes must not depend on them)
+  if (x6_mode(h)) feat.row_ash = ws.i((size_t)M);
+  if (feat.h2) feat.r.ash_row = feat.row_ash;  // scaled per row by the final LayerNorm (its exact row maxima)
   Act z;
   z.f = ws.f((size_t)M * c.vq_dim);
-  if (x6_mode(h)) z.p = ws.u16((size_t)M * c.vq_dim * 3);
-  z.h2 = z.p && h->has_gen && takes_h3_conv(h, h->conv_pre);  // conv_pre's input as the VQ up block writes it
+  // conv_pre's input: planes from the VQ up block's epilogue (x6), or in h3 split from z.f by the
+  // generator with each clip's exact range (launch_h2_ranged)
+  if (x6_mode(h) && !(h->has_gen && takes_h3_conv(h, h->conv_pre, T))) z.p = ws.u16((size_t)M * c.vq_dim * 3);
   const size_t mark = ws.off;
   size_t need = mark;
   auto sub = [&](auto fn) -> int {  // each sub-stage reuses the tail of the workspace
@@ -1630,10 +1896,12 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
   }
   if (match_idx(m, "encoder.downsample_layers.%d%n", &a) && a >= 1 && a < 4) {
     Act ln = conv_input(h, ws, (size_t)M * c.enc_dims[a - 1]);
+    if (x6_mode(h)) ln.row_ash = ws.i((size_t)M);
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
     ln.c1 = ln.p && takes_compact(h, h->ds_conv[a], M);
-    ln.h2 = ln.p && takes_h3(h, h->ds_conv[a]);
+    ln.h2 = ln.p && ln.row_ash && takes_h3(h, h->ds_conv[a]);
+    ln.r.ash_row = ln.h2 ? ln.row_ash : nullptr;
     RUN(run_ln(h, h->ds_ln[a], x, ln, M, s));
     ConvCall cd = pointwise(ln, M);
     cd.y = y;
@@ -1644,9 +1912,11 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
     const bool down = m == "quantizer.downsample.0";
     const int D = c.vq_dim;
     CAct in(x, nullptr);
-    RUN(ensure_planes(h, in, M, D, ws, s));
+    // the down conv in h3 as in the pipeline (range floor: the encoder's final LayerNorm bound)
+    RUN(ensure_planes(h, in, M, D, ws, s, false, down && takes_h3(h, h->vq_down), 0));
     Act ln = conv_input(h, ws, (size_t)M * D);
     Act hid = conv_input(h, ws, (size_t)M * 4 * D);
+    row_ranges(h, ws, M, ln, hid);
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
     ConvCall cc = pointwise(in, M);
@@ -1656,7 +1926,7 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
   }
   if (m == "quantizer.grvq.rvqs.0.project_in") {  // residual_vq.py:152
     CAct in(x, nullptr);
-    RUN(ensure_planes(h, in, M, c.vq_dim, ws, s, false, takes_h3(h, h->vq_pin)));
+    RUN(ensure_planes(h, in, M, c.vq_dim, ws, s, false, takes_h3(h, h->vq_pin), 0));
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
     ConvCall cp = pointwise(in, M);
@@ -1673,6 +1943,7 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
     if (!blk->C) return fail(h, DCX_ERR_STATE, "module weights not finalized");
     Act ln = conv_input(h, ws, (size_t)M * blk->C);
     Act hid = conv_input(h, ws, (size_t)M * 4 * blk->C);
+    row_ranges(h, ws, M, ln, hid);
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
     HIPCHK(h, hipMemcpyAsync(y, x, sizeof(float) * M * blk->C, hipMemcpyDeviceToDevice, s));
@@ -1708,7 +1979,7 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
   if (!h->has_gen && m.rfind("generator.", 0) == 0) return fail(h, DCX_ERR_STATE, "generator weights were not finalized");
   if (m == "generator.conv_pre") {  // generators.py:121
     CAct in(x, nullptr);
-    RUN(ensure_planes(h, in, M, c.vq_dim, ws, s, false, takes_h3_conv(h, h->conv_pre)));
+    RUN(ensure_planes(h, in, M, c.vq_dim, ws, s, false, takes_h3_conv(h, h->conv_pre, L), B));
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
     ConvCall cc = framed(in, B, L, c.vq_dim);
@@ -1732,42 +2003,68 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
   if (match_idx(m, "generator.ups.%d%n", &a) && a >= 0 && a < c.n_ups) {
     const ConvW& up = h->ups[a];
     CAct in(x, nullptr);
-    if (!(x6_mode(h) && f32_input_ok(up))) RUN(ensure_planes(h, in, M, up.cin, ws, s, false, takes_h3_conv(h, up)));
+    if (!(x6_mode(h) && f32_input_ok(up))) RUN(ensure_planes(h, in, M, up.cin, ws, s, false, takes_h3_conv(h, up, L), B));
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
     ConvCall cc = framed(in, B, L, up.cin);
     cc.y = y;
     return run_conv(h, up, cc, s);
   }
-  auto in_form = [&](const Act& v, const ConvW& consumer) -> Act {
-    if (!x6_mode(h) || !f32_input_ok(consumer)) return v;
-    return Act{v.f ? v.f : reinterpret_cast<float*>(v.p), nullptr};
-  };
+  auto in_form = [&](const Act& v, const ConvW& consumer) -> Act { return fp32_form(h, v, consumer); };
   // ResBlock1 (convnext_utils.py:106-113), as per-conv launches of the production conv kernels
   if (match_idx(m, "generator.resblocks.%d.blocks.%d%n", &a, &b) && a >= 0 && a < c.n_ups && b >= 0 && b < c.n_res) {
     const ConvW& w0 = h->res[a][b][0][0];
     const int C = w0.cout;
     Act XS = conv_input(h, ws, (size_t)M * C);  // silu(state), the c1 input (unless silu on load)
     Act Tb = conv_input(h, ws, (size_t)M * C);  // silu(c1 output)
+    RangeArena ra;
+    ra.reserve(ws, B);
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    HIPCHK(h, dcx::launch_zero_words(ra.base, (long long)RangeArena::kSlots * B, s));
     const bool silu_on_load = x6_mode(h) && f32_input_ok(w0);
     Act XSi = in_form(XS, w0), Tbi = in_form(Tb, w0);
-    XSi.h2 = Tbi.h2 = h3_stage(h, a);
+    XSi.h2 = Tbi.h2 = h3_stage(h, a, L);
     HIPCHK(h, hipMemcpyAsync(y, x, sizeof(float) * M * C, hipMemcpyDeviceToDevice, s));
-    if (!silu_on_load)
-      LAUNCH(h, s, "silu_act", 0, 10.0 * M * C, dcx::launch_silu_act(y, XSi.f, XSi.p, M, C, s, XSi.h2 ? 1 : 0));
+    Rng st;  // the state's range: its measured max |.| (and, in h2, its silu's shift)
+    st.amax = ra.amax();
+    if (!silu_on_load && XSi.h2) {
+      int* sh = ra.ash();
+      LAUNCH(h, s, "h2_ranged", 0, 12.0 * M * C,
+             dcx::launch_h2_ranged(y, nullptr, XSi.p, B, L, C, 1, 0.f, const_cast<float*>(st.amax), sh, h->rflag, s));
+      st.ash = sh;
+    } else {
+      LAUNCH(h, s, "clip_amax", 0, 4.0 * M * C, dcx::launch_clip_amax(y, B, L, C, const_cast<float*>(st.amax), s));
+      if (!silu_on_load)
+        LAUNCH(h, s, "silu_act", 0, 10.0 * M * C, dcx::launch_silu_act(y, XSi.f, XSi.p, M, C, s, 0));
+    }
     for (int ci = 0; ci < 3; ++ci) {
-      ConvCall c1 = framed(silu_on_load ? Act{y, nullptr} : XSi, B, L, C);
+      const ConvW& w1 = h->res[a][b][ci][0];
+      const ConvW& w2 = h->res[a][b][ci][1];
+      Act in1 = silu_on_load ? Act{y, nullptr} : XSi;
+      in1.r = st;
+      ConvCall c1 = framed(in1, B, L, C);
       c1.silu_in = silu_on_load;
       c1.silu_to(Tbi);
-      RUN(run_conv(h, h->res[a][b][ci][0], c1, s));
-      ConvCall c2 = framed(Tbi, B, L, C);
+      c1.yb = prog_conv(w1, st);
+      c1.y_amax = ra.amax();
+      c1.y_ash = Tbi.h2 ? ra.ash() : nullptr;
+      RUN(run_conv(h, w1, c1, s));
+      const Rng tr{c1.y_ash, 0, c1.y_amax, 0.f};
+      Act tin = Tbi;
+      tin.r = tr;
+      ConvCall c2 = framed(tin, B, L, C);
       c2.epi = dcx::EPI_RES;
       c2.res = y;
       c2.y = y;
       if (!silu_on_load && ci < 2) c2.silu_to(XSi);
-      RUN(run_conv(h, h->res[a][b][ci][1], c2, s));
+      c2.yb.c = w2.b_abs;  // |state + c2 + b2| <= max|state| + g2 max|c1 output| + max|b2|
+      prog_add(c2.yb, 1.0f, Rng{nullptr, 0, st.amax, 0.f});
+      prog_add(c2.yb, w2.g_abs, tr);
+      c2.y_amax = ra.amax();
+      c2.y_ash = !silu_on_load && ci < 2 && XSi.h2 ? ra.ash() : nullptr;
+      RUN(run_conv(h, w2, c2, s));
+      st = Rng{c2.y_ash, 0, c2.y_amax, 0.f};
     }
     return DCX_OK;
   }
@@ -1786,12 +2083,15 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
       RS[rb] = conv_input(h, ws, per);
       pb.Tb[rb] = conv_input(h, ws, per);
     }
+    RangeArena ra;
+    ra.reserve(ws, B);
     if (ws.dry) return DCX_OK;
     if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for the module");
+    HIPCHK(h, dcx::launch_zero_words(ra.base, (long long)RangeArena::kSlots * B, s));
     const bool silu_on_load = x6_mode(h) && f32_input_ok(w0);
     HIPCHK(h, hipMemcpyAsync(X, x, sizeof(float) * per, hipMemcpyDeviceToDevice, s));
     pb.X = X;
-    const bool h3 = h3_stage(h, a);
+    const bool h3 = h3_stage(h, a, L);
     pb.XS = in_form(XS, w0);
     pb.XS.h2 = h3;
     for (int rb = 0; rb < c.n_res; ++rb) {
@@ -1799,10 +2099,21 @@ int stage_module(dcx_codec* h, const std::string& m, const float* x, int B, int 
       pb.Tb_in[rb] = in_form(pb.Tb[rb], w0);
       pb.RS[rb].h2 = pb.Tb_in[rb].h2 = h3;
     }
-    if (!silu_on_load)
-      LAUNCH(h, s, "silu_act", 0, 10.0 * per, dcx::launch_silu_act(X, pb.XS.f, pb.XS.p, M, C, s, h3 ? 1 : 0));
+    float* amax_X = ra.amax();
+    if (!silu_on_load && h3) {
+      int* sh = ra.ash();
+      LAUNCH(h, s, "h2_ranged", 0, 12.0 * per,
+             dcx::launch_h2_ranged(X, nullptr, pb.XS.p, B, L, C, 1, 0.f, amax_X, sh, h->rflag, s));
+      pb.XS.r = Rng{sh, 0, amax_X, 0.f};
+    } else {
+      LAUNCH(h, s, "clip_amax", 0, 4.0 * per, dcx::launch_clip_amax(X, B, L, C, amax_X, s));
+      if (!silu_on_load)
+        LAUNCH(h, s, "silu_act", 0, 10.0 * per, dcx::launch_silu_act(X, pb.XS.f, pb.XS.p, M, C, s, 0));
+    }
     pb.Mx = y;
     pb.last = true;
+    pb.amax_X = amax_X;
+    pb.ra = &ra;
     return run_parallel_block(h, a, B, L, pb, s);
   }
   return fail(h, DCX_ERR_INVALID_ARG, "unknown module: " + m);
@@ -2061,6 +2372,11 @@ static int build_all(dcx_codec* h, Builder& B, int32_t with_generator) {
       hipFree(tmp);
       if (rc != DCX_OK) return rc;
     }
+    // the h3 range flags (round 6)
+    if (!B.bad() && !B.dry) {
+      h->rflag = (int*)B.alloc(1);
+      if (!h->rflag || hipMemset(h->rflag, 0, sizeof(int)) != hipSuccess) return fail(h, DCX_ERR_HIP, "range flag");
+    }
   }
   // ---- generator ------------------------------------------------------------------------
   if (with_generator) {
@@ -2285,10 +2601,33 @@ int dcx_set_split_k(dcx_codec* h, int32_t max_splits) {
 
 int dcx_set_knob(dcx_codec* h, const char* name, int32_t value) {
   if (!h || !name) return DCX_ERR_INVALID_ARG;
-  if (h->busy.load()) return fail(h, DCX_ERR_STATE, "dcx_set_knob during a stage call");
+  // claim the handle as a stage call does (CallScope), so no call starts while the knob changes
+  CallScope scope(h);
+  if (!scope.owner) return fail(h, DCX_ERR_STATE, "dcx_set_knob during a stage call");
   int* k = knob_slot(h->knobs, name);
   if (!k) return fail(h, DCX_ERR_INVALID_ARG, std::string("unknown knob: ") + name);
   *k = value;
+  return DCX_OK;
+}
+
+int dcx_get_knob(const dcx_codec* h, const char* name, int32_t* value) {
+  if (!h || !name || !value) return DCX_ERR_INVALID_ARG;
+  dcx::Knobs k = h->knobs;
+  const int* slot = knob_slot(k, name);
+  if (!slot) return DCX_ERR_INVALID_ARG;
+  *value = *slot;
+  return DCX_OK;
+}
+
+int dcx_range_flags(dcx_codec* h, int32_t* flags, int32_t reset) {
+  if (!h || !flags) return DCX_ERR_INVALID_ARG;
+  *flags = 0;
+  if (!h->rflag) return DCX_OK;  // not finalized: no h3 call has run
+  int v = 0;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&v, h->rflag, sizeof v, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(h, DCX_ERR_HIP, "reading the range flags failed");
+  *flags = v;
+  if (reset && hipMemset(h->rflag, 0, sizeof v) != hipSuccess) return fail(h, DCX_ERR_HIP, "resetting the range flags failed");
   return DCX_OK;
 }
 

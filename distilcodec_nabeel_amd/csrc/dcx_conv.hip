@@ -292,6 +292,24 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
   const long long ob = (long long)b * p.y_bstride;
   unsigned short* y6 = p.y6 ? p.y6 + ob * (p.y_compact == 1 ? 1 : p.y_compact >= 2 ? 2 : 3) : nullptr;
   unsigned short* y6s = p.y6s ? p.y6s + ob * (p.y6s_h2 ? 2 : 3) : nullptr;
+  // h2 output range (dcx_kernels.h h2_shift): the clip's scale from its bound program, the same in
+  // every workgroup of the clip, or (yb.rowwise, one-tap convs) each row's from its own bound
+  // (wave-uniform values moved to scalar registers: the accumulators still occupy most VGPRs here)
+  const bool h2o = (y6 && p.y_compact == 3) || (y6s && p.y6s_h2);
+  const bool h2row = h2o && p.yb.rowwise;
+  int osh = 0;
+  if (h2o && !h2row) {
+    const float bnd = range_bound(p.yb, b);
+    osh = __builtin_amdgcn_readfirstlane(h2_shift(bnd));
+    if (tid == 0) {
+      if (p.y_ash) p.y_ash[b] = osh;
+      if (p.rflag && !(bnd <= 3.0e38f)) atomicOr(p.rflag, RANGE_NONFINITE);
+    }
+  }
+  const float osc =
+      __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, __builtin_ldexpf(1.0f, osh))));
+  const bool track = p.y_amax || (h2o && p.rflag);
+  float vmax = 0.f;  // largest |v| this thread finishes (range_report)
   // Each thread finishes G consecutive output channels of a row (G = 8: 16-byte plane / compact
   // stores; the epilogue's store issue, not its bytes, sets its pace), the same channels for every
   // row, so bias and gamma are loaded once per tile.
@@ -384,13 +402,15 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
       const long long orow = (long long)q * p.out_mul + ph;
       const long long o = ob + orow * p.ldy + co;
       f32x4 x[NH];
+      // a one-tap h3 conv's input scaled per row: undo the row's power of two (exact) before the bias
+      const float rin = p.x_ash_row ? __builtin_ldexpf(1.0f, -p.x_ash_row[(long long)b * p.Lin + q]) : 1.0f;
       if constexpr (NH == 2) {
         const f32x4 u = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + cg + 4 * hsw);
         const f32x4 v = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + cg + 4 * (1 - hsw));
-        x[0] = (hsw ? v : u) + bias4[0];
-        x[1] = (hsw ? u : v) + bias4[1];
+        x[0] = (hsw ? v : u) * rin + bias4[0];
+        x[1] = (hsw ? u : v) * rin + bias4[1];
       } else {
-        x[0] = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + cg) + bias4[0];
+        x[0] = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + cg) * rin + bias4[0];
       }
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
@@ -448,6 +468,22 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
           if (p.round_bf16) x[h] = round_bf16x4(x[h]);
         }
       }
+      float rsc = osc;  // the h2 output's scale for this row
+      if (h2row) {
+        const long long grow = (long long)b * p.Lq + q;
+        const float bnd = range_bound(p.yb, grow);
+        const int sh = h2_shift(bnd);
+        rsc = __builtin_ldexpf(1.0f, sh);
+        if (cg == 0 && p.y_ash) p.y_ash[grow] = sh;
+        if (p.rflag && !(bnd <= 3.0e38f)) atomicOr(p.rflag, RANGE_NONFINITE);
+      }
+      if (track) {  // per-row scales: the scaled values against 65504 (range_report)
+        const float ts = h2row ? rsc : 1.0f;
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) vmax = fmaxf(vmax, fabsf(x[h][e]) * ts);
+      }
       if (p.y) {
 #pragma unroll
         for (int h = 0; h < NH; ++h) *reinterpret_cast<f32x4*>(p.y + o + 4 * h) = x[h];
@@ -459,7 +495,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
         if (y6) {
           if (p.y_compact == 1) store_bf16x8(y6, orow, p.Cout, co, xv);
           else if (p.y_compact == 2) store_hm8(y6, orow, p.Cout, co, xv);
-          else if (p.y_compact == 3) store_h2_8(y6, orow, p.Cout, co, xv);
+          else if (p.y_compact == 3) store_h2_8(y6, orow, p.Cout, co, xv, rsc);
           else store_planes8(y6, orow, p.Cout, co, xv);
         }
         if (p.y2 || y6s) {
@@ -471,7 +507,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
             *reinterpret_cast<f32x4*>(p.y2 + o + 4) = f32x4{sv[4], sv[5], sv[6], sv[7]};
           }
           if (y6s) {
-            if (p.y6s_h2) store_h2_8(y6s, orow, p.Cout, co, sv);
+            if (p.y6s_h2) store_h2_8(y6s, orow, p.Cout, co, sv, rsc);
             else store_planes8(y6s, orow, p.Cout, co, sv);
           }
         }
@@ -479,7 +515,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
         if (y6) {
           if (p.y_compact == 1) store_bf16x4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
           else if (p.y_compact == 2) store_hm4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
-          else if (p.y_compact == 3) store_h2_4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
+          else if (p.y_compact == 3) store_h2_4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3], rsc);
           else store_planes4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
         }
         if (p.y2 || y6s) {
@@ -488,7 +524,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
           for (int e = 0; e < 4; ++e) sv[e] = p.round_bf16 ? bf16_val(bf16_bits(silu_f(x[0][e]))) : silu_f(x[0][e]);
           if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
           if (y6s) {
-            if (p.y6s_h2) store_h2_4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+            if (p.y6s_h2) store_h2_4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3], rsc);
             else store_planes4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
           }
         }
@@ -516,6 +552,9 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
       for (int rb = 0; rb < ROWS_T; rb += IBF) batch(r0, rb, rb == 0, std::integral_constant<int, IBF>{});
     }
   }
+  // (rowwise: vmax holds scaled values, and y_amax is not recorded)
+  if (track) range_report(vmax, h2row ? nullptr : p.y_amax, b, h2row ? 65504.0f : h2o ? 65504.0f / osc : __builtin_inff(),
+                          p.rflag);  // workgroup-uniform
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -564,11 +603,15 @@ __device__ __forceinline__ void splitk_epi4(const ConvParams& p, const float* __
     x = (*reinterpret_cast<const f32x4*>(p.macc + o) + x) / 3.0f;
   }
   if (p.y) *reinterpret_cast<f32x4*>(p.y + o) = x;
+  // h2 outputs (not produced in the split-K mode, which runs no h3 conv; kept consistent): the clip's
+  // range scale (epilogue_lds); no maxima are recorded here
+  const float osc = (p.y6 && p.y_compact == 3) || (p.y6s && p.y6s_h2)
+                        ? __builtin_ldexpf(1.0f, h2_shift(range_bound(p.yb, b))) : 1.0f;
   if (p.y6) {
     unsigned short* y6 = p.y6 + ob * (p.y_compact == 1 ? 1 : p.y_compact >= 2 ? 2 : 3);
     if (p.y_compact == 1) store_bf16x4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
     else if (p.y_compact == 2) store_hm4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
-    else if (p.y_compact == 3) store_h2_4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
+    else if (p.y_compact == 3) store_h2_4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3], osc);
     else store_planes4(y6, orow, p.Cout, co, x[0], x[1], x[2], x[3]);
   }
   if (p.y2 || p.y6s) {
@@ -576,7 +619,7 @@ __device__ __forceinline__ void splitk_epi4(const ConvParams& p, const float* __
 #pragma unroll
     for (int e = 0; e < 4; ++e) sv[e] = silu_f(x[e]);
     if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
-    if (p.y6s && p.y6s_h2) store_h2_4(p.y6s + ob * 2, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
+    if (p.y6s && p.y6s_h2) store_h2_4(p.y6s + ob * 2, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3], osc);
     else if (p.y6s) store_planes4(p.y6s + ob * 3, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
   }
 }
@@ -2555,8 +2598,8 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, con
   }
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // undo the weight scaling (a power of two: exact)
-  const float unscale = __builtin_ldexpf(1.0f, -p.w3_shift);
+  // undo the weight and the input's range scaling (powers of two: exact)
+  const float unscale = __builtin_ldexpf(1.0f, -(p.w3_shift + (p.x_ash ? p.x_ash[b] : p.x_ash_c)));
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -2830,7 +2873,8 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
   }
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const float unscale = __builtin_ldexpf(1.0f, -p.w3_shift);
+  // undo the weight and the input's range scaling (powers of two: exact)
+  const float unscale = __builtin_ldexpf(1.0f, -(p.w3_shift + (p.x_ash ? p.x_ash[b] : p.x_ash_c)));
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll

@@ -20,6 +20,65 @@ enum Mean : int { MEAN_NONE = 0, MEAN_FIRST = 1, MEAN_MID = 2, MEAN_LAST = 3 };
 
 constexpr int kMaxPhases = 8;
 
+// ---- h3 activation range (round 6) ------------------------------------------------------------
+// An h2 pair (h = fp16(y), l = fp16(y - h)) carries 22 significant bits only while |y| lies in
+// [2^-3, 2^16): below, l goes subnormal (an absolute floor of 2^-25), above, fp16 saturates.  Every
+// h2 tensor is therefore stored as y = x * 2^a, with a = h2_shift(bound) chosen per clip from an
+// upper bound of |x| known BEFORE the tensor is produced (scaled bound in [2^14, 2^15): a 2x margin
+// under 65504), and its consumer multiplies its accumulators by 2^-(a + w3_shift) (exact).  Two
+// granularities:
+//  * per ROW for the one-tap (1x1) consumers, whose output row depends on one input row: a kernel
+//    that sees a whole row before splitting it (LayerNorm, launch_h2_rows) takes the row's exact max;
+//    the ConvNeXt MLP hidden takes G max|LayerNorm row| + max|bias| (RangeProg::rowwise);
+//  * per CLIP for the tap convs (the generator): G max|input| + max|bias| (+ max|residual|) with
+//    max|input| MEASURED per clip by the input's producer (ConvParams::y_amax), so the looseness of
+//    one layer never compounds; a caller's tensor by its exact clip max (launch_h2_ranged).
+// G is the largest absolute row sum of the weights (host).  All bounds are rigorous; with the bound
+// B the per-element error is at most 2^-22 |x| + 2^-39 B.
+constexpr int kH2Top = 15;
+constexpr int kH2ShiftMax = 64;
+__host__ __device__ inline int h2_shift(float bound) {
+  if (!(bound <= 3.0e38f)) return 0;  // NaN / inf bound: unscaled (the producer raises the range flag)
+  if (bound < 1e-30f) return kH2ShiftMax;
+  int e = 0;
+  (void)frexpf(bound, &e);  // bound = f 2^e, f in [0.5, 1): bound * 2^(15 - e) < 2^15
+  const int a = kH2Top - e;
+  return a < -kH2ShiftMax ? -kH2ShiftMax : a > kH2ShiftMax ? kH2ShiftMax : a;
+}
+// Range flag bits (dcx_range_flags): an h2 output's bound was not finite / a value exceeded it.
+enum RangeFlag : int { RANGE_NONFINITE = 1, RANGE_OVER = 2 };
+// Bound program of an h2 output, evaluated on the device before the tensor is written, per clip b
+// (or per row, rowwise: b = the launch's global row b * Lq + q):
+// c + sum_{i < n} g[i] * max(m[i] ? m[i][b] : 0, f[i]).  m: measured maxima; f: floors.
+constexpr int kRangeTerms = 6;
+struct RangeProg {
+  const float* m[kRangeTerms];
+  float g[kRangeTerms], f[kRangeTerms];
+  float c;
+  int n;
+  int rowwise;  // m indexed by row; the shift written per row (y_ash[row])
+};
+// (device) the program's bound for clip b; unrolled so the kernel-argument arrays are indexed
+// statically (a dynamic index would copy them to scratch)
+__device__ __forceinline__ float range_bound(const RangeProg& r, long long b) {
+  float v = r.c;
+#pragma unroll
+  for (int i = 0; i < kRangeTerms; ++i)
+    if (i < r.n) v += r.g[i] * fmaxf(r.m[i] ? r.m[i][b] : 0.f, r.f[i]);
+  return v;
+}
+// (device) a wave's largest |value| (vmax >= 0 per lane) into amax[b] (atomicMax on the fp32 bits,
+// which order like the values for non-negative floats), and RANGE_OVER when it exceeds lim (the
+// largest |value| the h2 output's scale admits; +inf when there is none).  One atomic per wave.
+__device__ __forceinline__ void range_report(float vmax, float* amax, int b, float lim, int* rflag) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off, 64));
+  if ((threadIdx.x & 63) == 0) {
+    if (amax) atomicMax(reinterpret_cast<unsigned*>(amax + b), __float_as_uint(vmax));
+    if (rflag && vmax > lim) atomicOr(rflag, RANGE_OVER);
+  }
+}
+
 // A/B and test switches.  dcx_create reads them from the environment ONCE into its handle
 // (knobs_from_env, dcx_api.cpp) and dcx_set_knob changes them per handle; no launcher reads the
 // environment, so a captured hipGraph and the eager calls after it run the same kernels.  Every
@@ -111,6 +170,18 @@ struct ConvParams {
   int w3_shift;
   // y6s in the h2 layout instead of planes (the input of a following h3 conv)
   int y6s_h2;
+  // h3 activation range (round 6, see h2_shift): the h2 input holds x * 2^x_ash[clip] (x_ash null:
+  // x_ash_c for every clip); an h2 output (y6 with y_compact == 3, or y6s with y6s_h2) is written as
+  // v * 2^h2_shift(yb(clip)) and that shift stored to y_ash[clip] (may be null); y_amax (may be null)
+  // receives the per-clip max |v| of the epilogue's final value v (atomicMax on the fp32 bits);
+  // rflag (may be null) the RangeFlag bits
+  const int* x_ash;
+  int x_ash_c;
+  const int* x_ash_row;  // one-tap convs: a per-row shift of the input row b * Lin + q (epilogue_lds)
+  int* y_ash;
+  float* y_amax;
+  RangeProg yb;
+  int* rflag;
 };
 
 // Independent convs issued as one launch (launch_conv_group); problem k owns logical tiles
@@ -162,6 +233,14 @@ struct ResPairParams {
   // h3 (conv_res_pair_h3): w1 / w2 are the ConvParams::w3 weights, scaled by 2^w3_shift{1,2}[m]
   int h3;
   int w3_shift1[kMaxGroup], w3_shift2[kMaxGroup];
+  // h3 activation range (round 6): member m's S image is silu(src) * 2^h2_shift(src_amax[m][clip]),
+  // its T image silu(c1 + b1) * 2^h2_shift(g1[m] src_amax[m][clip] + bm1[m]) (g1: the c1 weights'
+  // largest absolute row sum, bm1: max |b1|); dst_amax[m] (may be null) receives the per-clip max
+  // |dst| (atomicMax) for the next pair's S image.  src_amax null: 0 (x6 kernels ignore all of it).
+  const float* src_amax[kMaxGroup];
+  float* dst_amax[kMaxGroup];
+  float g1[kMaxGroup], bm1[kMaxGroup];
+  int* rflag;
   const Knobs* kn;  // host only; null = the defaults
 };
 
@@ -239,14 +318,30 @@ hipError_t launch_vq_reduce(const float* part_val, const int* part_idx, int rows
 hipError_t launch_row_sqnorm(const float* x, long long rows, int C, float* out, double* x2d, float* xr2,
                              unsigned long long* zero_me, hipStream_t s);
 // y6c: y6 in the compact bf16 layout instead of planes; channels_first_form: 0 F.layer_norm, 1 the
-// reference's channels_first LayerNorm, 2 the latter on a bf16 input under CUDA autocast
+// reference's channels_first LayerNorm, 2 the latter on a bf16 input under CUDA autocast.
+// An h2 output (y6c == 3) is scaled per row by 2^h2_shift(the row's max |output|), that shift stored
+// to ash_row[row] (required) and the max to amax_row[row] (may be null)
 hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, int y6c, const float* w, const float* b,
-                          long long rows, int C, float eps, int channels_first_form, hipStream_t s);
+                          long long rows, int C, float eps, int channels_first_form, hipStream_t s,
+                          int* ash_row = nullptr, float* amax_row = nullptr);
 // bf16: the reference's CUDA autocast (DCX_GEMM_BF16): input, taps and bias rounded to bf16, the
 // depthwise conv's result rounded to bf16, then the fp32 F.layer_norm
 hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6c, const float* dww, const float* dwb,
                             const float* lnw, const float* lnb, int batch, int L, int C, int bf16, const Knobs* kn,
-                            hipStream_t s);
+                            hipStream_t s, int* ash_row = nullptr, float* amax_row = nullptr);
+// fp32 [rows][C] -> h2, each row scaled by 2^h2_shift(its max |x|), the shift to ash_row[row] (the
+// input of a one-tap h3 conv handed in by the caller or written in fp32 by its producer)
+hipError_t launch_h2_rows(const float* x, unsigned short* y6, long long rows, int C, int* ash_row, hipStream_t s);
+// h3 activation range of a tensor handed in by the caller (round 6): amax[b] = max |x| over clip b's
+// rows (batch clips of L rows, C channels; amax zeroed here first), then y6 = h2 of f(x) * 2^a with
+// a = h2_shift(max(amax[b], floor)) stored to ash[b]; f = silu when silu != 0 (its |f(x)| <= |x|).
+// yf (may be null) receives f(x) in fp32.
+hipError_t launch_h2_ranged(const float* x, float* yf, unsigned short* y6, int batch, long long L, int C, int silu,
+                            float floor, float* amax, int* ash, int* rflag, hipStream_t s);
+// n 32-bit words zeroed by a kernel (capture-safe ordering; hipMemsetAsync is not used on the path)
+hipError_t launch_zero_words(void* p, long long n, hipStream_t s);
+// amax[b] = max |x| over clip b (batch clips of L rows, C channels), amax zeroed here first
+hipError_t launch_clip_amax(const float* x, int batch, long long L, int C, float* amax, hipStream_t s);
 // the CU count of the current device (cached per device, thread-safe)
 int device_cus();
 // x6 codebook planes -> the per-K32 hi/mid layout of vq_prefilter_bk ((dim / 32) * ncodes * 64 bf16)

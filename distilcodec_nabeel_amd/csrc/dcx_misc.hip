@@ -30,7 +30,8 @@ __device__ __forceinline__ float wave_sum(float v) {
 template <int NV>
 __device__ __forceinline__ void ln_finish(f32x4 (&v)[NV], int C, float eps, int cf, const float* __restrict__ w,
                                           const float* __restrict__ b, float* __restrict__ yrow,
-                                          unsigned short* __restrict__ y6, int y6c, long long row, int lane) {
+                                          unsigned short* __restrict__ y6, int y6c, long long row, int lane,
+                                          int* __restrict__ ash_row, float* __restrict__ amax_row) {
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
@@ -50,6 +51,8 @@ __device__ __forceinline__ void ln_finish(f32x4 (&v)[NV], int C, float eps, int 
   const float var = wave_sum(sq) / (float)C;
   const float den = sqrtf(var + eps);
   const float rstd = 1.0f / den;
+  f32x4 ov[NV];
+  float am = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (lane + 64 * i) * 4;
@@ -61,19 +64,39 @@ __device__ __forceinline__ void ln_finish(f32x4 (&v)[NV], int C, float eps, int 
     } else {
       o = (v[i] - mean) * rstd * wv + bv;
     }
+    ov[i] = o;
+    am = fmaxf(am, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
     if (yrow) *reinterpret_cast<f32x4*>(yrow + c) = o;
-    if (y6) {
-      if (y6c == 1) store_bf16x4(y6, row, C, c, o.x, o.y, o.z, o.w);
-      else if (y6c == 3) store_h2_4(y6, row, C, c, o.x, o.y, o.z, o.w);  // h3 input (conv_gemm_x3dm)
-      else store_planes4(y6, row, C, c, o.x, o.y, o.z, o.w);
+  }
+  if (!y6) return;
+  // h2 (an h3 one-tap consumer): the row scaled by 2^h2_shift(its exact max |o|), the shift and the
+  // max recorded per row (dcx_kernels.h)
+  float sc = 1.0f;
+  if (y6c == 3) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) am = fmaxf(am, __shfl_xor(am, off, 64));
+    const int sh = h2_shift(am);
+    sc = __builtin_ldexpf(1.0f, sh);
+    if (lane == 0) {
+      ash_row[row] = sh;
+      if (amax_row) amax_row[row] = am;
     }
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    const f32x4 o = ov[i];
+    if (y6c == 1) store_bf16x4(y6, row, C, c, o.x, o.y, o.z, o.w);
+    else if (y6c == 3) store_h2_4(y6, row, C, c, o.x, o.y, o.z, o.w, sc);
+    else store_planes4(y6, row, C, c, o.x, o.y, o.z, o.w);
   }
 }
 
 template <int NV>
 __global__ void __launch_bounds__(256) ln_rows_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                        unsigned short* __restrict__ y6, int y6c, const float* __restrict__ w,
-                                                       const float* __restrict__ b, long long rows, float eps, int cf) {
+                                                       const float* __restrict__ b, long long rows, float eps, int cf,
+                                                       int* ash_row, float* amax_row) {
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -81,17 +104,18 @@ __global__ void __launch_bounds__(256) ln_rows_kernel(const float* __restrict__ 
   f32x4 v[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) v[i] = *reinterpret_cast<const f32x4*>(x + row * C + (lane + 64 * i) * 4);
-  ln_finish<NV>(v, C, eps, cf, w, b, y ? y + row * C : nullptr, y6, y6c, row, lane);
+  ln_finish<NV>(v, C, eps, cf, w, b, y ? y + row * C : nullptr, y6, y6c, row, lane, ash_row, amax_row);
 }
 
 hipError_t launch_ln_rows(const float* x, float* y, unsigned short* y6, int y6c, const float* w, const float* b,
-                          long long rows, int C, float eps, int cf, hipStream_t s) {
+                          long long rows, int C, float eps, int cf, hipStream_t s, int* ash_row, float* amax_row) {
+  if (y6 && y6c == 3 && !ash_row) return hipErrorInvalidValue;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   switch (C) {
-    case 256: hipLaunchKernelGGL(ln_rows_kernel<1>, grid, block, 0, s, x, y, y6, y6c, w, b, rows, eps, cf); break;
-    case 512: hipLaunchKernelGGL(ln_rows_kernel<2>, grid, block, 0, s, x, y, y6, y6c, w, b, rows, eps, cf); break;
-    case 768: hipLaunchKernelGGL(ln_rows_kernel<3>, grid, block, 0, s, x, y, y6, y6c, w, b, rows, eps, cf); break;
-    case 1024: hipLaunchKernelGGL(ln_rows_kernel<4>, grid, block, 0, s, x, y, y6, y6c, w, b, rows, eps, cf); break;
+    case 256: hipLaunchKernelGGL(ln_rows_kernel<1>, grid, block, 0, s, x, y, y6, y6c, w, b, rows, eps, cf, ash_row, amax_row); break;
+    case 512: hipLaunchKernelGGL(ln_rows_kernel<2>, grid, block, 0, s, x, y, y6, y6c, w, b, rows, eps, cf, ash_row, amax_row); break;
+    case 768: hipLaunchKernelGGL(ln_rows_kernel<3>, grid, block, 0, s, x, y, y6, y6c, w, b, rows, eps, cf, ash_row, amax_row); break;
+    case 1024: hipLaunchKernelGGL(ln_rows_kernel<4>, grid, block, 0, s, x, y, y6, y6c, w, b, rows, eps, cf, ash_row, amax_row); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -110,7 +134,7 @@ __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict_
                                                          unsigned short* __restrict__ y6, int y6c,
                                                          const float* __restrict__ dww, const float* __restrict__ dwb,
                                                          const float* __restrict__ lnw, const float* __restrict__ lnb,
-                                                         int L, int tiles, int bf) {
+                                                         int L, int tiles, int bf, int* ash_row, float* amax_row) {
   constexpr int C = 256 * NV, C4 = C / 4, ROWS = DW_R + 6;
   __shared__ f32x4 tile[ROWS * C4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -164,7 +188,7 @@ __global__ void __launch_bounds__(256) dwconv_ln_kernel(const float* __restrict_
       if (bf) v[i] = round_bf16x4(v[i]);
     }
     const long long row = (long long)bidx * L + t;
-    ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y ? y + row * C : nullptr, y6, y6c, row, lane);
+    ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y ? y + row * C : nullptr, y6, y6c, row, lane, ash_row, amax_row);
   }
 }
 
@@ -181,7 +205,8 @@ __global__ void __launch_bounds__(256) dwconv_ln_run_kernel(const float* __restr
                                                              unsigned short* __restrict__ y6, int y6c,
                                                              const float* __restrict__ dww, const float* __restrict__ dwb,
                                                              const float* __restrict__ lnw, const float* __restrict__ lnb,
-                                                             int L, int runs, long long nruns, int bf) {
+                                                             int L, int runs, long long nruns, int bf, int* ash_row,
+                                                             float* amax_row) {
   constexpr int C = 256 * NV, C4 = C / 4, S = 7 + D;
   __shared__ f32x4 wsh[7 * C4];
   for (int i = threadIdx.x; i < 7 * C4; i += 256) {
@@ -240,7 +265,7 @@ __global__ void __launch_bounds__(256) dwconv_ln_run_kernel(const float* __restr
         if (bf) v[i] = round_bf16x4(v[i]);
       }
       const long long row = (long long)bidx * L + tk;
-      ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y ? y + row * C : nullptr, y6, y6c, row, lane);
+      ln_finish<NV>(v, C, 1e-6f, 0, lnw, lnb, y ? y + row * C : nullptr, y6, y6c, row, lane, ash_row, amax_row);
     }
   }
 }
@@ -248,22 +273,23 @@ __global__ void __launch_bounds__(256) dwconv_ln_run_kernel(const float* __restr
 template <int NV>
 static void launch_dwconv_ln_nv(const float* x, float* y, unsigned short* y6, int y6c, const float* dww,
                                 const float* dwb, const float* lnw, const float* lnb, int batch, int L, int rw, int bf,
-                                hipStream_t s) {
+                                hipStream_t s, int* ash_row, float* amax_row) {
   const int runs = (L + rw - 1) / rw;
   const long long nruns = (long long)batch * runs;
   const dim3 grid((unsigned)((nruns + 3) / 4)), block(256);
   constexpr int D = NV >= 4 ? 1 : 2;  // rows prefetched beyond the window (registers: 2 waves per SIMD at C = 1024)
   switch (rw) {
-    case 32: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 32, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns, bf); break;
-    case 16: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 16, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns, bf); break;
-    case 8: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 8, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns, bf); break;
-    default: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 4, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns, bf); break;
+    case 32: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 32, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns, bf, ash_row, amax_row); break;
+    case 16: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 16, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns, bf, ash_row, amax_row); break;
+    case 8: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 8, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns, bf, ash_row, amax_row); break;
+    default: hipLaunchKernelGGL((dwconv_ln_run_kernel<NV, 4, D>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, runs, nruns, bf, ash_row, amax_row); break;
   }
 }
 
 hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6c, const float* dww, const float* dwb,
                             const float* lnw, const float* lnb, int batch, int L, int C, int bf16, const Knobs* kn,
-                            hipStream_t s) {
+                            hipStream_t s, int* ash_row, float* amax_row) {
+  if (y6 && y6c == 3 && !ash_row) return hipErrorInvalidValue;
   const bool tiled = kn && kn->dwconv_tiled;  // A/B and tests: the round-2 tiled kernel (same bits)
   const long long rows = (long long)batch * L;
   // below 8192 rows (a streaming hop: 93 rows) the tiled kernel's 4-row tiles, one row per wave,
@@ -273,10 +299,10 @@ hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6
     const int rw = rows >= 2048LL * 32 ? 32 : rows >= 2048LL * 16 ? 16 : rows >= 2048LL * 8 ? 8 : 4;
     if ((long long)batch * ((L + rw - 1) / rw) / 4 >= (1LL << 31)) return hipErrorInvalidValue;
     switch (C) {
-      case 256: launch_dwconv_ln_nv<1>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, bf16, s); break;
-      case 512: launch_dwconv_ln_nv<2>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, bf16, s); break;
-      case 768: launch_dwconv_ln_nv<3>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, bf16, s); break;
-      case 1024: launch_dwconv_ln_nv<4>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, bf16, s); break;
+      case 256: launch_dwconv_ln_nv<1>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, bf16, s, ash_row, amax_row); break;
+      case 512: launch_dwconv_ln_nv<2>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, bf16, s, ash_row, amax_row); break;
+      case 768: launch_dwconv_ln_nv<3>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, bf16, s, ash_row, amax_row); break;
+      case 1024: launch_dwconv_ln_nv<4>(x, y, y6, y6c, dww, dwb, lnw, lnb, batch, L, rw, bf16, s, ash_row, amax_row); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -287,14 +313,14 @@ hipError_t launch_dwconv_ln(const float* x, float* y, unsigned short* y6, int y6
   if ((long long)batch * tiles >= (1LL << 31)) return hipErrorInvalidValue;
   dim3 grid((unsigned)(batch * tiles)), block(256);
   switch (C) {
-    case 256: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<1, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16);
-      else hipLaunchKernelGGL((dwconv_ln_kernel<1, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16); break;
-    case 512: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<2, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16);
-      else hipLaunchKernelGGL((dwconv_ln_kernel<2, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16); break;
-    case 768: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<3, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16);
-      else hipLaunchKernelGGL((dwconv_ln_kernel<3, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16); break;
-    case 1024: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<4, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16);
-      else hipLaunchKernelGGL((dwconv_ln_kernel<4, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16); break;
+    case 256: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<1, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16, ash_row, amax_row);
+      else hipLaunchKernelGGL((dwconv_ln_kernel<1, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16, ash_row, amax_row); break;
+    case 512: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<2, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16, ash_row, amax_row);
+      else hipLaunchKernelGGL((dwconv_ln_kernel<2, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16, ash_row, amax_row); break;
+    case 768: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<3, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16, ash_row, amax_row);
+      else hipLaunchKernelGGL((dwconv_ln_kernel<3, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16, ash_row, amax_row); break;
+    case 1024: if (small) hipLaunchKernelGGL((dwconv_ln_kernel<4, 4>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16, ash_row, amax_row);
+      else hipLaunchKernelGGL((dwconv_ln_kernel<4, 16>), grid, block, 0, s, x, y, y6, y6c, dww, dwb, lnw, lnb, L, tiles, bf16, ash_row, amax_row); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -372,10 +398,10 @@ hipError_t launch_spec_mag(const float* spec, float* mag, unsigned short* mag6, 
 }
 
 // silu(x) as fp32 and/or planes (dcx_module_forward's ResBlock / ParallelBlock entries: the
-// generator itself produces these in conv epilogues).  Same arithmetic as the epilogues' silu.
+// generator itself produces these in conv epilogues).  Same arithmetic as the epilogues' silu.  The
+// h2 layout goes through launch_h2_ranged (its range scale needs the clip's max first).
 __global__ void __launch_bounds__(256) silu_act_kernel(const float* __restrict__ x, float* __restrict__ yf,
-                                                        unsigned short* __restrict__ y6, long long rows, int C,
-                                                        int h2) {
+                                                        unsigned short* __restrict__ y6, long long rows, int C) {
   const long long total4 = rows * C / 4;
   for (long long i4 = (long long)blockIdx.x * 256 + threadIdx.x; i4 < total4; i4 += (long long)gridDim.x * 256) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(x + i4 * 4);
@@ -383,23 +409,136 @@ __global__ void __launch_bounds__(256) silu_act_kernel(const float* __restrict__
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = v[e] * __builtin_amdgcn_rcpf(1.0f + __expf(-v[e]));
     if (yf) *reinterpret_cast<f32x4*>(yf + i4 * 4) = f32x4{o[0], o[1], o[2], o[3]};
-    if (y6 && h2) store_h2_4(y6, (i4 * 4) / C, C, (int)((i4 * 4) % C), o[0], o[1], o[2], o[3]);
-    else if (y6) store_planes4(y6, (i4 * 4) / C, C, (int)((i4 * 4) % C), o[0], o[1], o[2], o[3]);
+    if (y6) store_planes4(y6, (i4 * 4) / C, C, (int)((i4 * 4) % C), o[0], o[1], o[2], o[3]);
   }
 }
 
 hipError_t launch_silu_act(const float* x, float* yf, unsigned short* y6, long long rows, int C, hipStream_t s, int h2) {
-  if (C % 8 || rows < 0 || (h2 && C % 32)) return hipErrorInvalidValue;
+  if (C % 8 || rows < 0 || (h2 && y6)) return hipErrorInvalidValue;
   const long long total4 = rows * C / 4;
   if (total4 == 0) return hipSuccess;
   const long long nb = (total4 + 255) / 256;
   const unsigned g = (unsigned)(nb < 8192 ? nb : 8192);
-  hipLaunchKernelGGL(silu_act_kernel, dim3(g), dim3(256), 0, s, x, yf, y6, rows, C, h2);
+  hipLaunchKernelGGL(silu_act_kernel, dim3(g), dim3(256), 0, s, x, yf, y6, rows, C);
+  return hipGetLastError();
+}
+
+// launch_h2_ranged (round 6): the range of a tensor handed in by the caller, per clip (blockIdx.y):
+// the max |x| over the clip, then the h2 split of f(x) * 2^h2_shift(max(amax, floor)).
+__global__ void __launch_bounds__(256) clip_amax_kernel(const float* __restrict__ x, long long n4, float* amax) {
+  const int b = blockIdx.y;
+  const f32x4* xb = reinterpret_cast<const f32x4*>(x) + (long long)b * n4;
+  float m = 0.f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const f32x4 v = xb[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  range_report(m, amax, b, __builtin_inff(), nullptr);
+}
+
+__global__ void __launch_bounds__(256) h2_ranged_kernel(const float* __restrict__ x, float* __restrict__ yf,
+                                                         unsigned short* __restrict__ y6, long long L, int C, int silu,
+                                                         float floor, const float* __restrict__ amax, int* ash,
+                                                         int* rflag) {
+  const int b = blockIdx.y;
+  const float bound = fmaxf(amax[b], floor);
+  const int sh = h2_shift(bound);
+  const float sc = __builtin_ldexpf(1.0f, sh);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ash[b] = sh;
+    if (rflag && !(bound <= 3.0e38f)) atomicOr(rflag, RANGE_NONFINITE);
+  }
+  const long long n4 = L * C / 4, base = (long long)b * L * C;
+  for (long long i4 = (long long)blockIdx.x * 256 + threadIdx.x; i4 < n4; i4 += (long long)gridDim.x * 256) {
+    const long long i = base + i4 * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + i);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = silu ? v[e] * __builtin_amdgcn_rcpf(1.0f + __expf(-v[e])) : v[e];
+    if (yf) *reinterpret_cast<f32x4*>(yf + i) = f32x4{o[0], o[1], o[2], o[3]};
+    store_h2_4(y6, i / C, C, (int)(i % C), o[0], o[1], o[2], o[3], sc);
+  }
+}
+
+// launch_h2_rows (round 6): one wave per row, C = 256 NV channels: the row's max |x|, then its h2
+// split scaled by 2^h2_shift(max) (the LayerNorm kernels' per-row form, for tensors in fp32)
+template <int NV>
+__global__ void __launch_bounds__(256) h2_rows_kernel(const float* __restrict__ x, unsigned short* __restrict__ y6,
+                                                       long long rows, int* __restrict__ ash_row) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int C = 256 * NV;
+  f32x4 v[NV];
+  float am = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    v[i] = *reinterpret_cast<const f32x4*>(x + row * C + (lane + 64 * i) * 4);
+    am = fmaxf(am, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) am = fmaxf(am, __shfl_xor(am, off, 64));
+  const int sh = h2_shift(am);
+  const float sc = __builtin_ldexpf(1.0f, sh);
+  if (lane == 0) ash_row[row] = sh;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) store_h2_4(y6, row, C, (lane + 64 * i) * 4, v[i].x, v[i].y, v[i].z, v[i].w, sc);
+}
+
+hipError_t launch_h2_rows(const float* x, unsigned short* y6, long long rows, int C, int* ash_row, hipStream_t s) {
+  if (!x || !y6 || !ash_row || rows < 0) return hipErrorInvalidValue;
+  if (rows == 0) return hipSuccess;
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  switch (C) {
+    case 256: hipLaunchKernelGGL(h2_rows_kernel<1>, grid, block, 0, s, x, y6, rows, ash_row); break;
+    case 512: hipLaunchKernelGGL(h2_rows_kernel<2>, grid, block, 0, s, x, y6, rows, ash_row); break;
+    case 768: hipLaunchKernelGGL(h2_rows_kernel<3>, grid, block, 0, s, x, y6, rows, ash_row); break;
+    case 1024: hipLaunchKernelGGL(h2_rows_kernel<4>, grid, block, 0, s, x, y6, rows, ash_row); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// Zeroes n 32-bit words with a kernel, not hipMemsetAsync: inside a hipGraph capture the kernel node
+// is ordered like every other launch (round 6: with memset nodes for the range slots, the second
+// replay of a captured hop read slots the first had left).
+__global__ void __launch_bounds__(256) zero_words_kernel(unsigned* p, long long n) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) p[i] = 0u;
+}
+
+hipError_t launch_zero_words(void* p, long long n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (!p) return hipErrorInvalidValue;
+  const long long nb = (n + 255) / 256;
+  hipLaunchKernelGGL(zero_words_kernel, dim3((unsigned)std::min<long long>(nb, 1024)), dim3(256), 0, s, (unsigned*)p, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_clip_amax(const float* x, int batch, long long L, int C, float* amax, hipStream_t s) {
+  if (C % 4 || L < 0 || batch < 1 || batch > 65535 || !amax) return hipErrorInvalidValue;
+  hipError_t e = launch_zero_words(amax, batch, s);
+  if (e != hipSuccess) return e;
+  const long long n4 = L * C / 4;
+  const unsigned gx = (unsigned)std::max<long long>(1, std::min<long long>((n4 + 255) / 256, std::max(1, 4096 / batch)));
+  if (n4 > 0) hipLaunchKernelGGL(clip_amax_kernel, dim3(gx, batch), dim3(256), 0, s, x, n4, amax);
+  return hipGetLastError();
+}
+
+hipError_t launch_h2_ranged(const float* x, float* yf, unsigned short* y6, int batch, long long L, int C, int silu,
+                            float floor, float* amax, int* ash, int* rflag, hipStream_t s) {
+  if (C % 32 || L < 0 || batch < 1 || batch > 65535 || !y6 || !amax || !ash) return hipErrorInvalidValue;
+  hipError_t e = launch_zero_words(amax, batch, s);
+  if (e != hipSuccess) return e;
+  const long long n4 = L * C / 4;
+  const long long nb = (n4 + 255) / 256;
+  const unsigned gx = (unsigned)std::max<long long>(1, std::min<long long>(nb, std::max(1, 4096 / batch)));
+  if (n4 > 0) hipLaunchKernelGGL(clip_amax_kernel, dim3(gx, batch), dim3(256), 0, s, x, n4, amax);
+  hipLaunchKernelGGL(h2_ranged_kernel, dim3(gx, batch), dim3(256), 0, s, x, yf, y6, L, C, silu, floor, amax, ash, rflag);
   return hipGetLastError();
 }
 
 // fp32 [rows][C] -> planes, or (compact) bf16 [rows][C] (boundary conversion for tensors handed in
-// by the caller).
+// by the caller; the h2 layout goes through launch_h2_ranged).
 __global__ void __launch_bounds__(256) split_planes_kernel(const float* __restrict__ x, unsigned short* __restrict__ y6,
                                                             long long rows, int C, int compact) {
   const long long total4 = rows * C / 4;
@@ -409,13 +548,12 @@ __global__ void __launch_bounds__(256) split_planes_kernel(const float* __restri
     const long long i = i4 * 4;
     if (compact == 1) store_bf16x4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
     else if (compact == 2) store_hm4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
-    else if (compact == 3) store_h2_4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
     else store_planes4(y6, i / C, C, (int)(i % C), v.x, v.y, v.z, v.w);
   }
 }
 
 hipError_t launch_split_planes(const float* x, unsigned short* y6, long long rows, int C, int compact, hipStream_t s) {
-  if (C % 8 || compact < 0 || compact > 3 || (compact >= 2 && C % 32)) return hipErrorInvalidValue;
+  if (C % 8 || compact < 0 || compact > 2 || (compact >= 2 && C % 32)) return hipErrorInvalidValue;
   const long long total4 = rows * C / 4;
   unsigned g = (unsigned)((total4 + 255) / 256);
   if (g > 8192) g = 8192;

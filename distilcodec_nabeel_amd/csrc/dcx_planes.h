@@ -134,20 +134,23 @@ __device__ __forceinline__ void store_hm8(unsigned short* base, long long row, i
   *reinterpret_cast<s16x8p*>(dst + 8) = mv;
 }
 
-// "h2" layout (the h3 arithmetic of conv_gemm_x3dq): x as two fp16 values, h = fp16(x) (RNE; |x| >
-// 65504 saturates to +-65504) and l = fp16(x - h) (x - h is exact in fp32), 22 significant bits
-// (l is exact to 2^-25 absolute where x - h is subnormal).  The hm layout's order: [rows][C/32][8
-// pieces][8] fp16, piece = ((c >> 3) & 3) * 2 + plane, 4 B per element.
+// "h2" layout (the h3 arithmetic of conv_gemm_x3dq): x as two fp16 values, h = fp16(x) (RNE) and
+// l = fp16(x - h) (x - h is exact in fp32), 22 significant bits for |x| in [2^-3, 2^16) (l is exact
+// to 2^-25 absolute where x - h is subnormal).  Producers scale x by 2^h2_shift(bound) first
+// (dcx_kernels.h), so the range is only left when a bound is violated: |x| > 65504 then saturates
+// to +-65504 with l = 0 (finite; the producer raises RANGE_OVER), NaN stays NaN.  The hm layout's
+// order: [rows][C/32][8 pieces][8] fp16, piece = ((c >> 3) & 3) * 2 + plane, 4 B per element.
 __device__ __forceinline__ void split2h(float x, unsigned short& h, unsigned short& l) {
   const float xs = fabsf(x) > 65504.f ? copysignf(65504.f, x) : x;  // NaN stays NaN
   const _Float16 hh = (_Float16)xs;
   h = __builtin_bit_cast(unsigned short, hh);
-  l = __builtin_bit_cast(unsigned short, (_Float16)(x - (float)hh));
+  l = __builtin_bit_cast(unsigned short, (_Float16)(xs - (float)hh));
 }
+// sc: the producer's power-of-two range scale (exact)
 __device__ __forceinline__ void store_h2_4(unsigned short* base, long long row, int C, int c, float a, float b,
-                                           float cc, float d) {
+                                           float cc, float d, float sc = 1.0f) {
   s16x4p hv, lv;
-  const float v[4] = {a, b, cc, d};
+  const float v[4] = {a * sc, b * sc, cc * sc, d * sc};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     unsigned short h, l;
@@ -159,12 +162,13 @@ __device__ __forceinline__ void store_h2_4(unsigned short* base, long long row, 
   *reinterpret_cast<s16x4p*>(dst) = hv;
   *reinterpret_cast<s16x4p*>(dst + 8) = lv;
 }
-__device__ __forceinline__ void store_h2_8(unsigned short* base, long long row, int C, int c, const float (&v)[8]) {
+__device__ __forceinline__ void store_h2_8(unsigned short* base, long long row, int C, int c, const float (&v)[8],
+                                           float sc = 1.0f) {
   s16x8p hv, lv;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     unsigned short h, l;
-    split2h(v[e], h, l);
+    split2h(v[e] * sc, h, l);
     hv[e] = (short)h;
     lv[e] = (short)l;
   }

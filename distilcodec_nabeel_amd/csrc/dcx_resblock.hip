@@ -754,7 +754,8 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
     pf[k][0] = q[0];
     pf[k][1] = q[1];
   };
-  auto commit_fill = [&](int r0) {
+  // sc: the image's range scale, 2^h2_shift(max |state| of the clip) (dcx_kernels.h)
+  auto commit_fill = [&](int r0, float sc) {
 #pragma unroll
     for (int k = 0; k < NIT; ++k) {
       const int it = tid + 512 * k;
@@ -765,7 +766,7 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
       s16x8 hv, lv;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float sv = rp_silu(pf[k][e >> 2][e & 3]);
+        const float sv = rp_silu(pf[k][e >> 2][e & 3]) * sc;
         const float v = ok ? sv : 0.f;
         unsigned short hh, ll;
         split2h(v, hh, ll);
@@ -840,6 +841,12 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
   auto no_hook = [] {};
 
   const int nrb2 = min(RB, (G::NB2 - wr + WR - 1) / WR);
+  // range shifts (round 6): member m's S image of clip bb from the measured max |state|, its T image
+  // from the bound g1 max|state| + max|b1| of c1's output (|silu(v)| <= |v|)
+  auto s_shift = [&](int m, int bb) { return p.src_amax[m] ? h2_shift(p.src_amax[m][bb]) : 0; };
+  auto t_shift = [&](int m, int bb) {
+    return p.src_amax[m] ? h2_shift(fmaf(p.g1[m], p.src_amax[m][bb], p.bm1[m])) : 0;
+  };
   int tile = blockIdx.x;
   if (tile >= total) return;  // whole workgroup, before any barrier
   int b = tile / ntl, r0 = (tile - b * ntl) * R;
@@ -851,7 +858,7 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
   for (int ch = 0; ch < NCH; ++ch) load_wf(p.w1[0], ch);
 #pragma unroll
   for (int k = 0; k < NIT; ++k) issue_fill_item(p.src[0] + (long long)b * p.bstride, r0, k);
-  commit_fill(r0);
+  commit_fill(r0, __builtin_ldexpf(1.0f, s_shift(0, b)));
   rp_barrier();
   f32x4 macc[MEAN ? RB : 1][2];
 #ifdef RP_DIAG_STAMPS
@@ -878,8 +885,11 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
       }
       RP_T(tb);
       rp_barrier();  // every wave's S reads are done before T overwrites them
-      // ---- T image: silu(c1 + b1) as h / l over the S image (zero outside the clip)
-      const float us1 = __builtin_ldexpf(1.0f, -p.w3_shift1[m]);
+      // ---- T image: silu(c1 + b1) as h / l over the S image (zero outside the clip), range-scaled
+      const int sh_t = t_shift(m, b);
+      const float us1 = __builtin_ldexpf(1.0f, -(p.w3_shift1[m] + s_shift(m, b)));
+      const float tsc = __builtin_ldexpf(1.0f, sh_t), tlim = 65504.0f / tsc;
+      float tmax = 0.f;
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
@@ -891,8 +901,10 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
           s16x4 hv, lv;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float sv = rp_silu(acc[i][cb][e] * us1 + bias[e]);
-            const float v = ok ? sv : 0.f;
+            const float pre = acc[i][cb][e] * us1 + bias[e];
+            const float sv = rp_silu(pre);
+            const float v = ok ? sv * tsc : 0.f;
+            if (ok) tmax = fmaxf(tmax, fabsf(pre));
             unsigned short hh, ll;
             split2h(v, hh, ll);
             hv[e] = (short)hh;
@@ -903,6 +915,7 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
           *reinterpret_cast<s16x4*>(dst + 4 * PS) = lv;
         }
       }
+      if (p.rflag) range_report(tmax, nullptr, b, tlim, p.rflag);  // workgroup-uniform
       rp_barrier();
       RP_T(tc);
       // ---- c2 over rows [r0, r0 + R) from the T image.  Tap 0 loads the residual rows, taps 1 and 2
@@ -946,8 +959,10 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
         if (ts && (j + 1) % ts == 0 && j + 1 < k) rp_barrier();
       }
       RP_T(te);
-      // ---- epilogue: state + c2 + b2 (rows past the clip end are dropped)
-      const float us2 = __builtin_ldexpf(1.0f, -p.w3_shift2[m]);
+      // ---- epilogue: state + c2 + b2 (rows past the clip end are dropped); its max |.| per clip for
+      // the next pair's S image
+      const float us2 = __builtin_ldexpf(1.0f, -(p.w3_shift2[m] + sh_t));
+      float dmax = 0.f;
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
@@ -958,7 +973,10 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
           const int q = r0 + (wr + WR * i) * 16 + l15;
           const f32x4 v = res[i][cb] + (acc[i][cb] * us2 + bias);
           if constexpr (!MEAN) {
-            if (q < L) *reinterpret_cast<f32x4*>(p.dst[m] + cb0 + (long long)q * C + c0) = v;
+            if (q < L) {
+              *reinterpret_cast<f32x4*>(p.dst[m] + cb0 + (long long)q * C + c0) = v;
+              dmax = fmaxf(dmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+            }
           } else if (m == 0) {
             macc[i][cb] = v;
           } else if (!last_m) {
@@ -972,10 +990,13 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
           }
         }
       }
+      if constexpr (!MEAN) {
+        if (p.dst_amax[m]) range_report(dmax, p.dst_amax[m], b, __builtin_inff(), nullptr);  // workgroup-uniform
+      }
       RP_T(tf);
       if (has_next) {
         rp_barrier();  // every wave's T reads are done before the next S image overwrites them
-        commit_fill(nsr0);
+        commit_fill(nsr0, __builtin_ldexpf(1.0f, last_m ? s_shift(0, nb) : s_shift(m + 1, b)));
         rp_barrier();
       }
 #ifdef RP_DIAG_STAMPS

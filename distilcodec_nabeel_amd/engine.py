@@ -140,17 +140,31 @@ class NativeCodec:
         variables dcx_create reads once).  Takes effect for later calls on this engine."""
         self._check(self.L.dcx_set_knob(self.h, name.encode(), int(value)))
 
+    def get_knob(self, name: str) -> int:
+        """The current value of a switch (dcx_get_knob)."""
+        v = ctypes.c_int32(0)
+        self._check(self.L.dcx_get_knob(self.h, name.encode(), ctypes.byref(v)))
+        return v.value
+
     @contextlib.contextmanager
     def knobs(self, **values):
-        """Switches set for the calls inside the block, then back to the shipped defaults
-        (KNOB_DEFAULTS): `with eng.knobs(DCX_RP_OLD=1): ...`."""
+        """Switches set for the calls inside the block, then back to the values they had before
+        (an environment override given at creation included): `with eng.knobs(DCX_RP_OLD=1): ...`."""
+        saved = {k: self.get_knob(k) for k in values}
         for k, v in values.items():
             self.set_knob(k, v)
         try:
             yield self
         finally:
-            for k in values:
-                self.set_knob(k, KNOB_DEFAULTS[k])
+            for k, v in saved.items():
+                self.set_knob(k, v)
+
+    def range_flags(self, reset: bool = False) -> int:
+        """The h3 range flags (dcx_range_flags; synchronises): bit 0 a non-finite operand bound, bit 1
+        a saturated h3 operand.  0 for every finite input."""
+        v = ctypes.c_int32(0)
+        self._check(self.L.dcx_range_flags(self.h, ctypes.byref(v), int(reset)))
+        return v.value
 
     def num_frames(self, n_samples: int) -> int:
         return int(self.L.dcx_num_frames(self.h, n_samples))

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define DCX_ABI_VERSION 3
+#define DCX_ABI_VERSION 4
 
 enum {
   DCX_OK = 0,
@@ -168,8 +168,21 @@ int64_t dcx_mp3_bad_frames(void);
 int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int64_t cols, void* stream);
 
 /* Arithmetic of every contraction (convs, linears, STFT, mel, VQ distances):
- *  DCX_GEMM_X6  (default) fp32 operands split into three bf16 planes, six exact bf16 products per
- *               fp32 product, fp32 accumulation on v_mfma_f32_32x32x16_bf16 (fp32-level accuracy);
+ *  DCX_GEMM_X6  (default) fp32-tolerance emulation on the matrix cores, two forms:
+ *               "x6": fp32 operands split into three bf16 planes (24 significant bits, the full fp32
+ *               exponent range), six exact bf16 products per fp32 product, fp32 accumulation on
+ *               v_mfma_f32_16x16x32_bf16 / 32x32x16_bf16 (the mel front end, the stem, the ConvTs
+ *               and the VQ distance prefilter);
+ *               "h3" (round 5; DCX_H3 / DCX_H3_1X1 / DCX_H3_PAIRS below): operands as two fp16
+ *               values (22 significant bits), three exact fp16 products per fp32 product, fp32
+ *               accumulation on v_mfma_f32_16x16x32_f16 (the generator's ResBlock convs, conv_pre,
+ *               the wide ConvTs, the ConvNeXt 1x1 convs).  Each h3 operand tensor is scaled per clip
+ *               by a power of two chosen from a rigorous bound of its values (round 6), so the fp16
+ *               range covers it whatever the input scale; a violated bound (only with inf / NaN
+ *               inputs) saturates and sets a flag (dcx_range_flags).
+ *               Both forms are held to the fp32 tolerance of the product contract (tests/test_gpu_h3.py,
+ *               tests/test_gpu_range.py: module outputs within 2e-4 relative of fp64 at input scales
+ *               2^-12 .. 2^12); neither is IEEE fp32 arithmetic (that is DCX_GEMM_F32);
  *  DCX_GEMM_F32 v_mfma_f32_32x32x2_f32 (IEEE fp32 fma chain);
  *  DCX_GEMM_BF16 the reference's enable_bfloat16 (torch.autocast bf16, distil_codec.py:550): conv /
  *               linear operands rounded to bf16, one bf16 product, fp32 accumulation, results
@@ -201,6 +214,14 @@ int dcx_set_split_k(dcx_codec* h, int32_t max_splits);
  * Unset, every switch selects the shipped path.  DCX_ERR_INVALID_ARG for an unknown name,
  * DCX_ERR_STATE during a stage call. */
 int dcx_set_knob(dcx_codec* h, const char* name, int32_t value);
+/* The current value of a switch (DCX_ERR_INVALID_ARG for an unknown name). */
+int dcx_get_knob(const dcx_codec* h, const char* name, int32_t* value);
+
+/* h3 range flags (round 6; see DCX_GEMM_X6): bit 0 = an h3 operand's bound was not finite (an inf /
+ * NaN upstream), bit 1 = a value exceeded its bound and saturated (never for finite inputs: the
+ * bounds are rigorous).  Cumulative over the handle's calls; synchronises the device; reset != 0
+ * clears them. */
+int dcx_range_flags(dcx_codec* h, int32_t* flags, int32_t reset);
 
 /* Standalone 1-D convolution primitive (the kernel family behind every stage), for tests and
  * benchmarks.  weight: host fp32, Conv1d layout [Cout][Cin][k] (transposed=0) or

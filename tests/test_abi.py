@@ -28,7 +28,7 @@ def test_header_symbols_exported_and_bound():
         assert hasattr(L, n), n
         assert n in _native.SIGNATURES, f"{n} has no ctypes signature"
     assert set(_native.SIGNATURES) == set(names)
-    assert L.dcx_abi_version() == 3
+    assert L.dcx_abi_version() == 4
 
 
 def test_config_struct_matches_default(cfg):
