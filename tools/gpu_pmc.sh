@@ -1,7 +1,7 @@
-# GPU-box: SQ counter passes over C3 (bf16: vq_prefilter_b1, conv_gemm_bf16dm) and C2 (the ResBlock
-# pair kernels and the conv family), plus FETCH/WRITE over C3.  Usage: bash tools/gpu_pmc_r04.sh TAG
+# GPU-box: SQ counter passes over C3 (bf16: vq_prefilter_b1, conv_gemm_bf16dm / bf16dp) and C2 (the h3 kernels, the ResBlock
+# pair kernels and the conv family), plus FETCH/WRITE over C3.  Usage: bash tools/gpu_pmc.sh TAG
 set -o pipefail
-TAG=${1:-pmc4}
+TAG=${1:-pmc5}
 R=${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp; cd $R
 PASSES=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAVES"
@@ -18,5 +18,7 @@ run c3_write WRITE_SIZE python3 tools/c3_bench.py --gemm bf16 --steps 1 --warmup
 for i in 0 1 2; do run c2_p$i "${PASSES[$i]}" python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-f32 --no-profile --no-c3 --no-c4 --no-c5 --no-oracle-codes; done
 python3 tools/pmc_summary.py $R/gpurun_out/${TAG}_c3_p0 $R/gpurun_out/${TAG}_c3_p1 $R/gpurun_out/${TAG}_c3_p2 $R/gpurun_out/${TAG}_c3_fetch $R/gpurun_out/${TAG}_c3_write > $R/gpurun_out/${TAG}_c3_summary.txt
 python3 tools/pmc_summary.py $R/gpurun_out/${TAG}_c2_p0 $R/gpurun_out/${TAG}_c2_p1 $R/gpurun_out/${TAG}_c2_p2 > $R/gpurun_out/${TAG}_c2_summary.txt
-grep -A 30 "vq_prefilter_b1\|conv_gemm_bf16dm" $R/gpurun_out/${TAG}_c3_summary.txt | grep -E "^dcx|MFMA busy|WAIT_ANY /|ACTIVE_INST_ANY /|FETCH|WRITE" | head -40
-grep -A 30 "conv_res_pair" $R/gpurun_out/${TAG}_c2_summary.txt | grep -E "^dcx|MFMA busy|WAIT_ANY /|ACTIVE_INST_ANY /" | head -40
+python3 tools/pmc_table.py $R/gpurun_out/${TAG}_c3_summary.txt > $R/gpurun_out/${TAG}_c3_table.md
+python3 tools/pmc_table.py $R/gpurun_out/${TAG}_c2_summary.txt > $R/gpurun_out/${TAG}_c2_table.md
+cat $R/gpurun_out/${TAG}_c3_table.md $R/gpurun_out/${TAG}_c2_table.md
+grep -A 30 "vq_prefilter_b1\|conv_gemm_bf16d" $R/gpurun_out/${TAG}_c3_summary.txt | grep -E "^dcx|FETCH|WRITE" | head -20

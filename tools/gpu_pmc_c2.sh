@@ -1,4 +1,4 @@
-# GPU-box: the three SQ counter passes of tools/gpu_pmc_r05.sh over C2 only (the h3 kernels, the
+# GPU-box: the three SQ counter passes of tools/gpu_pmc.sh over C2 only (the h3 kernels, the
 # ResBlock pair kernels, the conv family).  Usage: bash tools/gpu_pmc_c2.sh TAG
 set -o pipefail
 TAG=${1:-pmc_c2}
