@@ -741,6 +741,7 @@ int* knob_slot(dcx::Knobs& k, const std::string& n) {
   if (n == "DCX_H3_1X1") return &k.h3_1x1;
   if (n == "DCX_H3_SPLIT") return &k.h3_split;
   if (n == "DCX_H3_PAIRS") return &k.h3_pairs;
+  if (n == "DCX_RP_RING") return &k.rp_ring;
   return nullptr;
 }
 
@@ -749,7 +750,7 @@ void knobs_from_env(dcx::Knobs& k) {
                                       "DCX_RP_W4",        "DCX_GELU_LUT",     "DCX_BF16_PERSIST", "DCX_BF16_REG_EPI",
                                       "DCX_DWCONV_TILED", "DCX_SPLIT_MIN_STEPS", "DCX_SPLIT_GROUP_OFF",
                                       "DCX_H3",           "DCX_H3_BN",        "DCX_H3_1X1",
-                                      "DCX_H3_SPLIT",     "DCX_H3_PAIRS"};
+                                      "DCX_H3_SPLIT",     "DCX_H3_PAIRS",     "DCX_RP_RING"};
   for (const char* n : names) {
     const char* e = std::getenv(n);
     if (e && *e) *knob_slot(k, n) = std::atoi(e);

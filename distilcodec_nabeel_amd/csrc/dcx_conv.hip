@@ -274,9 +274,15 @@ extern "C" int dcx_diag_tiles(unsigned long long* out, int max_tiles, int reset)
 // stores).  This keeps the per-element code out of the 64-way unrolled accumulator loop.
 // ---------------------------------------------------------------------------------------------
 // acc: f32x16[WR/32][WC/32] (32x32 MFMA blocks) or f32x4[WR/16][WC/16] (16x16 blocks).
-template <int BM, int BN, int WM, int WN, int LDS_FLOATS, int NT, typename AccT>
-__device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int q0, int co0, int b, int ph,
-                                             float* smem) {
+// RROW: which per-row range forms a kernel may meet (round 6).  Bit 0: an h2 input scaled per row
+// (x_ash_row: the h3 one-tap kernels), loaded with the batch's rows; bit 1: a rowwise bound of an h2
+// output (yb.rowwise: one-tap kernels).  Tap convs pass 0, which keeps these registers out of their
+// epilogues (with them, round 6's first form spilled ~290 SGPRs into VGPR lanes in
+// conv_gemm_x3dw_group: +5 % on the dominant kernel).  pr: where the range fields are read (the
+// kernel argument itself in grouped launches, whose private copy then leaves them out).
+template <int BM, int BN, int WM, int WN, int LDS_FLOATS, int NT, int RROW = 2, typename AccT>
+__device__ __forceinline__ void epilogue_lds(const ConvParams& p, const ConvParams& pr, AccT& acc, int q0, int co0,
+                                             int b, int ph, float* smem) {
   constexpr int WR = BM / WM, WC = BN / WN;
   constexpr int TM = WR / 32, TN = WC / 32;
   constexpr bool M16 = sizeof(acc[0][0]) == 16;
@@ -293,22 +299,24 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
   unsigned short* y6 = p.y6 ? p.y6 + ob * (p.y_compact == 1 ? 1 : p.y_compact >= 2 ? 2 : 3) : nullptr;
   unsigned short* y6s = p.y6s ? p.y6s + ob * (p.y6s_h2 ? 2 : 3) : nullptr;
   // h2 output range (dcx_kernels.h h2_shift): the clip's scale from its bound program, the same in
-  // every workgroup of the clip, or (yb.rowwise, one-tap convs) each row's from its own bound
+  // every workgroup of the clip, or (pr.yb.rowwise, one-tap convs) each row's from its own bound
   // (wave-uniform values moved to scalar registers: the accumulators still occupy most VGPRs here)
   const bool h2o = (y6 && p.y_compact == 3) || (y6s && p.y6s_h2);
-  const bool h2row = h2o && p.yb.rowwise;
+  constexpr bool RIN = RROW & 1, ROUT = RROW & 2;
+  const bool h2row = ROUT && h2o && pr.yb.rowwise;
   int osh = 0;
   if (h2o && !h2row) {
-    const float bnd = range_bound(p.yb, b);
+    const float bnd = range_bound(pr.yb, b);
     osh = __builtin_amdgcn_readfirstlane(h2_shift(bnd));
     if (tid == 0) {
-      if (p.y_ash) p.y_ash[b] = osh;
-      if (p.rflag && !(bnd <= 3.0e38f)) atomicOr(p.rflag, RANGE_NONFINITE);
+      if (pr.y_ash) pr.y_ash[b] = osh;
+      if (pr.rflag && !(bnd <= 3.0e38f)) atomicOr(pr.rflag, RANGE_NONFINITE);
     }
   }
   const float osc =
       __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, __builtin_ldexpf(1.0f, osh))));
-  const bool track = p.y_amax || (h2o && p.rflag);
+  const bool track = pr.y_amax || (h2o && pr.rflag);
+  const float acur = track && !h2row ? range_cur(pr.y_amax, b) : 0.f;  // the clip's running max (range_report)
   float vmax = 0.f;  // largest |v| this thread finishes (range_report)
   // Each thread finishes G consecutive output channels of a row (G = 8: 16-byte plane / compact
   // stores; the epilogue's store issue, not its bytes, sets its pace), the same channels for every
@@ -393,6 +401,19 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
 #pragma unroll
         for (int h = 0; h < NH; ++h) m[k][h] = *reinterpret_cast<const f32x4*>(p.macc + lofs(k) + 4 * h);
     }
+    // per-row range data of a one-tap h3 conv (the input row's shift, the output row's bound), loaded
+    // with the batch's other rows: inside the row loop each was a memory round trip
+    // (a rowwise program has one term: prog_conv_rows)
+    auto row_bound = [&](int q) { return fmaf(pr.yb.g[0], fmaxf(pr.yb.m[0][(long long)b * p.Lq + q], pr.yb.f[0]), pr.yb.c); };
+    float rin[RIN ? IB : 1], rbnd[RIN ? IB : 1];
+    if constexpr (RIN) {
+#pragma unroll
+      for (int k = 0; k < IB; ++k) {
+        const int q = min(q0 + r0 + trow + (rb + k) * RSTEP, p.Lq - 1);
+        rin[k] = pr.x_ash_row ? __builtin_ldexpf(1.0f, -pr.x_ash_row[(long long)b * p.Lin + q]) : 1.0f;
+        rbnd[k] = h2row ? row_bound(q) : 0.f;
+      }
+    }
     if (stage) stage_acc(r0);
 #pragma unroll
     for (int k = 0; k < IB; ++k) {
@@ -403,14 +424,14 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
       const long long o = ob + orow * p.ldy + co;
       f32x4 x[NH];
       // a one-tap h3 conv's input scaled per row: undo the row's power of two (exact) before the bias
-      const float rin = p.x_ash_row ? __builtin_ldexpf(1.0f, -p.x_ash_row[(long long)b * p.Lin + q]) : 1.0f;
+      const float rin_ = RIN ? rin[RIN ? k : 0] : 1.0f;
       if constexpr (NH == 2) {
         const f32x4 u = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + cg + 4 * hsw);
         const f32x4 v = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + cg + 4 * (1 - hsw));
-        x[0] = (hsw ? v : u) * rin + bias4[0];
-        x[1] = (hsw ? u : v) * rin + bias4[1];
+        x[0] = (hsw ? v : u) * rin_ + bias4[0];
+        x[1] = (hsw ? u : v) * rin_ + bias4[1];
       } else {
-        x[0] = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + cg) * rin + bias4[0];
+        x[0] = *reinterpret_cast<const f32x4*>(smem + rl * LDSW + cg) * rin_ + bias4[0];
       }
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
@@ -471,11 +492,11 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
       float rsc = osc;  // the h2 output's scale for this row
       if (h2row) {
         const long long grow = (long long)b * p.Lq + q;
-        const float bnd = range_bound(p.yb, grow);
+        const float bnd = RIN ? rbnd[RIN ? k : 0] : row_bound(q);
         const int sh = h2_shift(bnd);
         rsc = __builtin_ldexpf(1.0f, sh);
-        if (cg == 0 && p.y_ash) p.y_ash[grow] = sh;
-        if (p.rflag && !(bnd <= 3.0e38f)) atomicOr(p.rflag, RANGE_NONFINITE);
+        if (cg == 0 && pr.y_ash) pr.y_ash[grow] = sh;
+        if (pr.rflag && !(bnd <= 3.0e38f)) atomicOr(pr.rflag, RANGE_NONFINITE);
       }
       if (track) {  // per-row scales: the scaled values against 65504 (range_report)
         const float ts = h2row ? rsc : 1.0f;
@@ -495,7 +516,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
         if (y6) {
           if (p.y_compact == 1) store_bf16x8(y6, orow, p.Cout, co, xv);
           else if (p.y_compact == 2) store_hm8(y6, orow, p.Cout, co, xv);
-          else if (p.y_compact == 3) store_h2_8(y6, orow, p.Cout, co, xv, rsc);
+          else if (p.y_compact == 3) store_h2_8<false>(y6, orow, p.Cout, co, xv, rsc);
           else store_planes8(y6, orow, p.Cout, co, xv);
         }
         if (p.y2 || y6s) {
@@ -507,7 +528,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
             *reinterpret_cast<f32x4*>(p.y2 + o + 4) = f32x4{sv[4], sv[5], sv[6], sv[7]};
           }
           if (y6s) {
-            if (p.y6s_h2) store_h2_8(y6s, orow, p.Cout, co, sv, rsc);
+            if (p.y6s_h2) store_h2_8<false>(y6s, orow, p.Cout, co, sv, rsc);
             else store_planes8(y6s, orow, p.Cout, co, sv);
           }
         }
@@ -515,7 +536,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
         if (y6) {
           if (p.y_compact == 1) store_bf16x4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
           else if (p.y_compact == 2) store_hm4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
-          else if (p.y_compact == 3) store_h2_4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3], rsc);
+          else if (p.y_compact == 3) store_h2_4<false>(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3], rsc);
           else store_planes4(y6, orow, p.Cout, co, x[0][0], x[0][1], x[0][2], x[0][3]);
         }
         if (p.y2 || y6s) {
@@ -524,7 +545,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
           for (int e = 0; e < 4; ++e) sv[e] = p.round_bf16 ? bf16_val(bf16_bits(silu_f(x[0][e]))) : silu_f(x[0][e]);
           if (p.y2) *reinterpret_cast<f32x4*>(p.y2 + o) = sv;
           if (y6s) {
-            if (p.y6s_h2) store_h2_4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3], rsc);
+            if (p.y6s_h2) store_h2_4<false>(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3], rsc);
             else store_planes4(y6s, orow, p.Cout, co, sv[0], sv[1], sv[2], sv[3]);
           }
         }
@@ -552,9 +573,9 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, AccT& acc, int
       for (int rb = 0; rb < ROWS_T; rb += IBF) batch(r0, rb, rb == 0, std::integral_constant<int, IBF>{});
     }
   }
-  // (rowwise: vmax holds scaled values, and y_amax is not recorded)
-  if (track) range_report(vmax, h2row ? nullptr : p.y_amax, b, h2row ? 65504.0f : h2o ? 65504.0f / osc : __builtin_inff(),
-                          p.rflag);  // workgroup-uniform
+  // (rowwise: vmax holds scaled values, and pr.y_amax is not recorded)
+  if (track) range_report(vmax, h2row ? nullptr : pr.y_amax, b, h2row ? 65504.0f : h2o ? 65504.0f / osc : __builtin_inff(),
+                          pr.rflag, acur);  // workgroup-uniform
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -933,7 +954,7 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const ConvParams p) {
   if constexpr (ARGMIN)
     epilogue<BM, BN, WM, WN, true>(p, acc, q0, co0, nt, ntiles, b, ph, smem);
   else
-    epilogue_lds<BM, BN, WM, WN, 2 * (BM + BN) * LDSK, 256>(p, acc, q0, co0, b, ph, smem);
+    epilogue_lds<BM, BN, WM, WN, 2 * (BM + BN) * LDSK, 256>(p, p, acc, q0, co0, b, ph, smem);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1238,7 +1259,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) conv_gemm_x6w8(const ConvPara
       setup(Ln);
       prologue_loads();
     }
-    epilogue_lds<BM, BN, WM, WN, (2 * ABUF + 3 * BBUF) / 2, NT>(p, acc, eq0, eco0, eb, eph,
+    epilogue_lds<BM, BN, WM, WN, (2 * ABUF + 3 * BBUF) / 2, NT, HALO ? 0 : 2>(p, p, acc, eq0, eco0, eb, eph,
                                                                 reinterpret_cast<float*>(lds));
     if (!more) break;
     L = Ln;
@@ -1274,7 +1295,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) conv_gemm_x6w8(const ConvPara
 // waves with the same 64 x 64 wave tiles, so the staging VALU of one group overlaps the other
 // group's MFMAs.
 template <int HALO, int BN, bool AF32 = false>
-__device__ __forceinline__ void x6pp_tile(const ConvParams& p, const int wg, const int b, const int ph) {
+__device__ __forceinline__ void x6pp_tile(const ConvParams& p, const ConvParams& pr, const int wg, const int b, const int ph) {
   // wave tiles 64 x (BN / 2): 24 MFMAs per segment at BN = 128
   static_assert(BN == 128 || BN == 256 || (AF32 && BN == 64), "column tile");
   constexpr int BM = AF32 ? 512 : 256, WN = AF32 ? 1 : 2, WM = 8 / WN;
@@ -1547,7 +1568,7 @@ __device__ __forceinline__ void x6pp_tile(const ConvParams& p, const int wg, con
     atomicAdd(&g_clock_diag[2], (unsigned long long)nsteps);
   }
 #endif
-  epilogue_lds<BM, BN, WM, WN, (2 * ABUF + 2 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+  epilogue_lds<BM, BN, WM, WN, (2 * ABUF + 2 * BBUF) / 2, 512, HALO ? 0 : 2>(p, pr, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1800,7 +1821,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6lm(const ConvParams p) {
     atomicAdd(&g_clock_diag[2], (unsigned long long)nsteps);
   }
 #endif
-  epilogue_lds<BM, BN, 4, WN, (2 * ABUF + 2 * BBUF) / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+  epilogue_lds<BM, BN, 4, WN, (2 * ABUF + 2 * BBUF) / 2, 512, HALO ? 0 : 2>(p, p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
 template <int HALO, int BN, bool AF32 = false>
@@ -1808,7 +1829,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp(const ConvParams p) {
   constexpr int BM = AF32 ? 512 : 256;
   int wg, b, ph;
   flat_tile(((p.Lq + BM - 1) / BM) * (p.Cout / BN), p.batch, wg, b, ph);
-  x6pp_tile<HALO, BN, AF32>(p, wg, b, ph);
+  x6pp_tile<HALO, BN, AF32>(p, p, wg, b, ph);
 }
 
 // Grouped split-K launch (round 4, the split-K latency mode): up to 3 independent halo convs (the
@@ -1820,11 +1841,12 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6pp_group(const ConvGroup g
   const int k = t >= g.start[1] ? (t >= g.start[2] ? 2 : 1) : 0;
   const int local = xcd_remap(t - g.start[k], g.start[k + 1] - g.start[k]);
   const int b = local / g.tiles_per_clip[k];
-  ConvParams p;  // a private copy (see conv_gemm_x6dq_group)
+  ConvParams p;  // a private copy of the main-loop fields (pr: the range fields, read in place by the epilogue)
   if (k == 0) p = g.p[0];
   else if (k == 1) p = g.p[1];
   else p = g.p[2];
-  x6pp_tile<64, 128>(p, local - b * g.tiles_per_clip[k], b, 0);
+  const ConvParams& pr = k == 0 ? g.p[0] : k == 1 ? g.p[1] : g.p[2];
+  x6pp_tile<64, 128>(p, pr, local - b * g.tiles_per_clip[k], b, 0);
 }
 
 template <int HALO>
@@ -2081,7 +2103,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6dm(const ConvParams p) {
     atomicAdd(&g_clock_diag[2], 2ull * nsteps);
   }
 #endif
-  epilogue_lds<BM, BN, 4, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+  epilogue_lds<BM, BN, 4, WN, LDS_US / 2, 512, HALO ? 0 : 2>(p, p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2105,7 +2127,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6dm(const ConvParams p) {
 // ---------------------------------------------------------------------------------------------
 // One output tile (wg = row tile * column tiles + column tile, clip b, phase ph).
 template <int BN>
-__device__ __forceinline__ void x6dq_tile(const ConvParams& p, const int wg, const int b, const int ph) {
+__device__ __forceinline__ void x6dq_tile(const ConvParams& p, const ConvParams& pr, const int wg, const int b, const int ph) {
   DCX_TILET(tile_t0);
   constexpr int HALO = 64;
   constexpr int BM = 65536 / BN, WN = 2;
@@ -2320,7 +2342,7 @@ __device__ __forceinline__ void x6dq_tile(const ConvParams& p, const int wg, con
   }
 #endif
   DCX_TILET(tile_t2);
-  epilogue_lds<BM, BN, 4, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+  epilogue_lds<BM, BN, 4, WN, LDS_US / 2, 512, 0>(p, pr, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 #ifdef DCX_TILE_DIAG
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -2341,7 +2363,7 @@ template <int BN>
 __global__ void __launch_bounds__(512, 2) conv_gemm_x6dq(const ConvParams p) {
   int wg, b, ph;
   flat_tile(((p.Lq + 65536 / BN - 1) / (65536 / BN)) * (p.Cout / BN), p.batch, wg, b, ph);
-  x6dq_tile<BN>(p, wg, b, ph);
+  x6dq_tile<BN>(p, p, wg, b, ph);
 }
 
 // Grouped launch: up to 3 independent convs with the same tiling (the three ResBlocks' convs of one
@@ -2357,11 +2379,12 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x6dq_group(const ConvGroup g
   const int b = local / g.tiles_per_clip[k];
   // a private copy: the tile body's inline-asm barriers clobber memory, which would make the
   // compiler re-read every field of a kernarg-resident struct after each of them
-  ConvParams p;
+  ConvParams p;  // a private copy of the main-loop fields (pr: the range fields, read in place by the epilogue)
   if (k == 0) p = g.p[0];
   else if (k == 1) p = g.p[1];
   else p = g.p[2];
-  x6dq_tile<BN>(p, local - b * g.tiles_per_clip[k], b, 0);
+  const ConvParams& pr = k == 0 ? g.p[0] : k == 1 ? g.p[1] : g.p[2];
+  x6dq_tile<BN>(p, pr, local - b * g.tiles_per_clip[k], b, 0);
 }
 
 template <int BN>
@@ -2403,7 +2426,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 // HALO = 0 (conv_gemm_x3dm): one-tap convs, every step opens a chunk, so the input tiles ride the
 // weight ring's 3 slots, over a descriptor of the tile's rows only (32-bit offsets at any length).
 template <int BN, int HALO>
-__device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, const int b, const int ph) {
+__device__ __forceinline__ void x3dq_tile(const ConvParams& p, const ConvParams& pr, const int wg, const int b, const int ph) {
   constexpr int BM = 32768 / BN, WN = BN / 64, WM = 8 / WN;
   constexpr int NA = HALO ? 2 : 3;
   constexpr int WR = BM / WM, WC = BN / WN, TM = WR / 16, TN = WC / 16;
@@ -2599,19 +2622,19 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const int wg, con
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // undo the weight and the input's range scaling (powers of two: exact)
-  const float unscale = __builtin_ldexpf(1.0f, -(p.w3_shift + (p.x_ash ? p.x_ash[b] : p.x_ash_c)));
+  const float unscale = __builtin_ldexpf(1.0f, -(p.w3_shift + (pr.x_ash ? pr.x_ash[b] : pr.x_ash_c)));
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] *= unscale;
-  epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+  epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512, HALO == 0 ? 3 : 0>(p, pr, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
 template <int BN, int HALO>
 __global__ void __launch_bounds__(512, 2) conv_gemm_x3dq(const ConvParams p) {
   int wg, b, ph;
   flat_tile(((p.Lq + 32768 / BN - 1) / (32768 / BN)) * (p.Cout / BN), p.batch, wg, b, ph);
-  x3dq_tile<BN, HALO>(p, wg, b, ph);
+  x3dq_tile<BN, HALO>(p, p, wg, b, ph);
 }
 
 // grouped launch of up to 3 h3 convs (conv_gemm_x6dq_group's member mapping)
@@ -2621,11 +2644,12 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x3dq_group(const ConvGroup g
   const int k = t >= g.start[1] ? (t >= g.start[2] ? 2 : 1) : 0;
   const int local = xcd_remap(t - g.start[k], g.start[k + 1] - g.start[k]);
   const int b = local / g.tiles_per_clip[k];
-  ConvParams p;
+  ConvParams p;  // a private copy of the main-loop fields (pr: the range fields, read in place by the epilogue)
   if (k == 0) p = g.p[0];
   else if (k == 1) p = g.p[1];
   else p = g.p[2];
-  x3dq_tile<BN, 64>(p, local - b * g.tiles_per_clip[k], b, 0);
+  const ConvParams& pr = k == 0 ? g.p[0] : k == 1 ? g.p[1] : g.p[2];
+  x3dq_tile<BN, 64>(p, pr, local - b * g.tiles_per_clip[k], b, 0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2658,7 +2682,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x3dq_group(const ConvGroup g
 // BN = 256: 256 x 256 tiles of 64 x 128 wave tiles (Cout % 256 == 0); BN = 128: 384 x 128 tiles of
 // 48 x 128 wave tiles (the C = 128 stage: 72 MFMAs per segment against x3dq's 48).
 template <int HALO, bool SPLIT, int BN = 256>
-__device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, const int b, const int ph) {
+__device__ __forceinline__ void x3dw_tile(const ConvParams& p, const ConvParams& pr, const int wg, const int b, const int ph) {
   constexpr int BM = BN == 256 ? 256 : 384, WN = BN / 128, WM = 8 / WN;
   constexpr int WR = BM / WM, WC = 128, TM = WR / 16, TN = WC / 16;
   constexpr int AR = BM + HALO;                 // rows of an input image
@@ -2874,12 +2898,12 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const int wg, con
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // undo the weight and the input's range scaling (powers of two: exact)
-  const float unscale = __builtin_ldexpf(1.0f, -(p.w3_shift + (p.x_ash ? p.x_ash[b] : p.x_ash_c)));
+  const float unscale = __builtin_ldexpf(1.0f, -(p.w3_shift + (pr.x_ash ? pr.x_ash[b] : pr.x_ash_c)));
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] *= unscale;
-  epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+  epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512, HALO == 0 ? 3 : 0>(p, pr, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
 }
 
 template <int HALO, bool SPLIT, int BN = 256>
@@ -2887,7 +2911,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x3dw(const ConvParams p) {
   constexpr int BM = BN == 256 ? 256 : 384;
   int wg, b, ph;
   flat_tile(((p.Lq + BM - 1) / BM) * (p.Cout / BN), p.batch, wg, b, ph);
-  x3dw_tile<HALO, SPLIT, BN>(p, wg, b, ph);
+  x3dw_tile<HALO, SPLIT, BN>(p, p, wg, b, ph);
 }
 
 template <bool SPLIT, int BN = 256>
@@ -2896,11 +2920,12 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_x3dw_group(const ConvGroup g
   const int k = t >= g.start[1] ? (t >= g.start[2] ? 2 : 1) : 0;
   const int local = xcd_remap(t - g.start[k], g.start[k + 1] - g.start[k]);
   const int b = local / g.tiles_per_clip[k];
-  ConvParams p;
+  ConvParams p;  // a private copy of the main-loop fields (pr: the range fields, read in place by the epilogue)
   if (k == 0) p = g.p[0];
   else if (k == 1) p = g.p[1];
   else p = g.p[2];
-  x3dw_tile<64, SPLIT, BN>(p, local - b * g.tiles_per_clip[k], b, 0);
+  const ConvParams& pr = k == 0 ? g.p[0] : k == 1 ? g.p[1] : g.p[2];
+  x3dw_tile<64, SPLIT, BN>(p, pr, local - b * g.tiles_per_clip[k], b, 0);
 }
 
 // Whether conv_gemm_x3dq<bn> (taps >= 3 with a halo) or conv_gemm_x3dm<bn> (one tap) takes an h3
@@ -3123,7 +3148,7 @@ __global__ void __launch_bounds__(512, 2) conv_gemm_bf16dm(const ConvParams p) {
       }
     }
   } else {
-    epilogue_lds<BM, BN, WM, WN, LDS_US / 2, 512>(p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+    epilogue_lds<BM, BN, WM, WN, LDS_US / 2, 512>(p, p, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
   }
 #ifdef DCX_TILE_DIAG
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

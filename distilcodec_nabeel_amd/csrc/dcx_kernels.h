@@ -67,14 +67,23 @@ __device__ __forceinline__ float range_bound(const RangeProg& r, long long b) {
     if (i < r.n) v += r.g[i] * fmaxf(r.m[i] ? r.m[i][b] : 0.f, r.f[i]);
   return v;
 }
+// (device) the current value of a running maximum slot (agent-scope atomic load: never a value newer
+// than the slot's, possibly an older one, which only costs an atomic that was not needed)
+__device__ __forceinline__ float range_cur(const float* amax, long long b) {
+  return amax ? __hip_atomic_load(amax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+}
 // (device) a wave's largest |value| (vmax >= 0 per lane) into amax[b] (atomicMax on the fp32 bits,
 // which order like the values for non-negative floats), and RANGE_OVER when it exceeds lim (the
-// largest |value| the h2 output's scale admits; +inf when there is none).  One atomic per wave.
-__device__ __forceinline__ void range_report(float vmax, float* amax, int b, float lim, int* rflag) {
+// largest |value| the h2 output's scale admits; +inf when there is none).  At most one atomic per
+// wave, and none when vmax does not exceed cur (range_cur of the slot, read earlier): the slots of
+// all clips share one cache line, so every wave's atomic serialised in one L2 channel, and each
+// later vmcnt wait of the wave (they count in issue order) waited behind it (round 6: C2 171 -> 181 ms
+// before this test).
+__device__ __forceinline__ void range_report(float vmax, float* amax, int b, float lim, int* rflag, float cur = -1.f) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off, 64));
   if ((threadIdx.x & 63) == 0) {
-    if (amax) atomicMax(reinterpret_cast<unsigned*>(amax + b), __float_as_uint(vmax));
+    if (amax && vmax > cur) atomicMax(reinterpret_cast<unsigned*>(amax + b), __float_as_uint(vmax));
     if (rflag && vmax > lim) atomicOr(rflag, RANGE_OVER);
   }
 }
@@ -100,6 +109,7 @@ struct Knobs {
   int h3_split = 1;         // DCX_H3_SPLIT=0: conv_gemm_x3dw's DMA issued by group 0 alone (A/B)
   int h3_pairs = 1;         // DCX_H3_PAIRS=0: the C = 32 / 64 ResBlock pairs in x6 arithmetic (A/B, tests)
   int h3_1x1 = 1;           // DCX_H3_1X1=0: the ConvNeXt blocks' 1x1 convs in x6 arithmetic (A/B, tests)
+  int rp_ring = 1;          // DCX_RP_RING=0: conv_res_pair_h3's weights loaded per wave instead of the LDS ring (A/B)
 };
 
 // out[b][q*out_mul + phase][co] = epi( sum_{m<taps} sum_{ci<Cin} x[b][q + in_base[phase] + m*in_step][ci]

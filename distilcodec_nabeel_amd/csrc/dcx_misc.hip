@@ -433,7 +433,7 @@ __global__ void __launch_bounds__(256) clip_amax_kernel(const float* __restrict_
     const f32x4 v = xb[i];
     m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
   }
-  range_report(m, amax, b, __builtin_inff(), nullptr);
+  range_report(m, amax, b, __builtin_inff(), nullptr, range_cur(amax, b));
 }
 
 __global__ void __launch_bounds__(256) h2_ranged_kernel(const float* __restrict__ x, float* __restrict__ yf,

@@ -140,13 +140,20 @@ __device__ __forceinline__ void store_hm8(unsigned short* base, long long row, i
 // (dcx_kernels.h), so the range is only left when a bound is violated: |x| > 65504 then saturates
 // to +-65504 with l = 0 (finite; the producer raises RANGE_OVER), NaN stays NaN.  The hm layout's
 // order: [rows][C/32][8 pieces][8] fp16, piece = ((c >> 3) & 3) * 2 + plane, 4 B per element.
+// SAT = false (split2h_nc): no saturation, for producers whose scale comes from a rigorous bound
+// and that report a violated one themselves (the conv epilogues and pair-kernel images: |x| <= 2^15
+// for finite inputs; past it h and l go inf / NaN and the producer has raised the range flag).  The
+// three VALU of the clamp were a tenth of those epilogues' per-element work.
+template <bool SAT = true>
 __device__ __forceinline__ void split2h(float x, unsigned short& h, unsigned short& l) {
-  const float xs = fabsf(x) > 65504.f ? copysignf(65504.f, x) : x;  // NaN stays NaN
+  const float xs = !SAT ? x : fabsf(x) > 65504.f ? copysignf(65504.f, x) : x;  // NaN stays NaN
   const _Float16 hh = (_Float16)xs;
   h = __builtin_bit_cast(unsigned short, hh);
   l = __builtin_bit_cast(unsigned short, (_Float16)(xs - (float)hh));
 }
+__device__ __forceinline__ void split2h_nc(float x, unsigned short& h, unsigned short& l) { split2h<false>(x, h, l); }
 // sc: the producer's power-of-two range scale (exact)
+template <bool SAT = true>
 __device__ __forceinline__ void store_h2_4(unsigned short* base, long long row, int C, int c, float a, float b,
                                            float cc, float d, float sc = 1.0f) {
   s16x4p hv, lv;
@@ -154,7 +161,7 @@ __device__ __forceinline__ void store_h2_4(unsigned short* base, long long row, 
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     unsigned short h, l;
-    split2h(v[e], h, l);
+    split2h<SAT>(v[e], h, l);
     hv[e] = (short)h;
     lv[e] = (short)l;
   }
@@ -162,13 +169,14 @@ __device__ __forceinline__ void store_h2_4(unsigned short* base, long long row, 
   *reinterpret_cast<s16x4p*>(dst) = hv;
   *reinterpret_cast<s16x4p*>(dst + 8) = lv;
 }
+template <bool SAT = true>
 __device__ __forceinline__ void store_h2_8(unsigned short* base, long long row, int C, int c, const float (&v)[8],
                                            float sc = 1.0f) {
   s16x8p hv, lv;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     unsigned short h, l;
-    split2h(v[e] * sc, h, l);
+    split2h<SAT>(v[e] * sc, h, l);
     hv[e] = (short)h;
     lv[e] = (short)l;
   }

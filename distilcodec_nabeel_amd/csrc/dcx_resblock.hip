@@ -728,14 +728,24 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_g(const ResPairParams p)
 // ((chunk * 8 + piece) * NS + row) * 16, piece = plane * 4 + channel group).  Weights: the
 // ConvParams::w3 tap slices ([chunk][Cout][4][h' 8 | l' 8], scaled by 2^w3_shift per conv); the
 // accumulators are scaled back before the bias.  Schedule, tiles and hand-offs are conv_res_pair_g's.
-template <int C, bool MEAN, int RR = kRp3Rows<C>>
+template <int C, bool MEAN, int RR = kRp3Rows<C>, bool RING = false>
 __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p) {
+#ifdef __HIP_DEVICE_COMPILE__  // the body is device code only (its host pass dropped the RING stubs)
   using G = RpGeom3<C, RR>;
   constexpr int R = G::R, WR = G::WR, RB = G::RB1, PS = G::PS;
   constexpr int G8 = G::G8, NIT = G::NIT, NS = G::NS;
   constexpr int NCH = G::NCH, IMG = G::IMG, WTAP = G::WTAP;
-  __shared__ __attribute__((aligned(16))) char lds[IMG + 2 * kMaxGroup * C * 4];
-  float* const bias_lds = reinterpret_cast<float*>(lds + IMG);  // [conv][member][C]
+  // RING (round 6, Knobs::rp_ring): the weight taps through an LDS ring of NSLOT taps instead of
+  // per-wave loads (below)
+  constexpr int NSLOT = 4, RINGB = RING ? NSLOT * WTAP : 0, BIASB = 2 * kMaxGroup * C * 4;
+  constexpr int NP = C * C / 256, PPW = (NP + 7) / 8;  // 1 KiB pieces per tap, per wave
+  static_assert(IMG + RINGB + BIASB + 2 * NSLOT * 4 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char lds[IMG + RINGB + BIASB + (RING ? 2 * NSLOT * 4 : 0)];
+  float* const bias_lds = reinterpret_cast<float*>(lds + IMG + RINGB);  // [conv][member][C]
+  // ring counters: rd_cnt[slot] += 1 per wave once it holds a tap of the slot in registers, full_cnt[slot]
+  // += 1 per wave once its pieces of the slot's tap have landed (monotone: use u of a slot is complete at 8 (u + 1))
+  unsigned* const rd_cnt = reinterpret_cast<unsigned*>(lds + IMG + RINGB + BIASB);
+  unsigned* const full_cnt = rd_cnt + NSLOT;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wc = wave % G::WC, wr = wave / G::WC;
@@ -769,7 +779,7 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
         const float sv = rp_silu(pf[k][e >> 2][e & 3]) * sc;
         const float v = ok ? sv : 0.f;
         unsigned short hh, ll;
-        split2h(v, hh, ll);
+        split2h_nc(v, hh, ll);
         hv[e] = (short)hh;
         lv[e] = (short)ll;
       }
@@ -783,7 +793,11 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
   // [column block][h' | l'] of the lane's channel group ----
   s16x8 wf[NCH][2][2];
   const int wo0 = ((2 * wc) * 16 + l15) * 128 + kg * 32, wo1 = wo0 + 16;
+  [[maybe_unused]] bool wl_off = false;  // -DRP_DIAG_NOWLOAD (timing only, wrong results): no reloads after the prologue
   auto load_wf = [&](const unsigned short* wtap, int ch) {
+#ifdef RP_DIAG_NOWLOAD
+    if (wl_off) return;
+#endif
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)wtap, 0, WTAP, 0x00020000);
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
@@ -795,9 +809,82 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
   // the tap after tap j of conv `conv` of member m: the stream runs c1, c2 of each member, then
   // member 0 again (the next tile; past the last tile harmless loads of weights already used)
   auto next_tap = [&](int m, int conv, int j) -> const unsigned short* {
+    if (RING) return nullptr;
     if (j + 1 < p.taps[m]) return (conv ? p.w2[m] : p.w1[m]) + (long long)(j + 1) * (WTAP / 2);
     if (conv == 0) return p.w2[m];
     return p.w1[m + 1 < nmem ? m + 1 : 0];
+  };
+
+  // ---- RING: the weight stream through LDS.  Tap t (counted over the whole kernel: c1 then c2 of
+  // each member, tile after tile) sits in slot t % NSLOT as NP pieces of 1 KiB, piece (ch, column
+  // block, h' | l') laid out as the fragment read of a wave (lane l: channel l & 15 of the block, K
+  // group l >> 4), so every ds_read_b128 of a fragment is one linear 1 KiB piece (conflict-free).
+  // Each wave issues pieces w, w + 8, ... of a tap by LDS-DMA, two taps ahead; per tap t it
+  //   A. counts itself in rd_cnt[t % NSLOT] once its reads of tap t (made during tap t - 1) returned;
+  //   B. waits for its own pieces of tap t + 1 (vmcnt, counted past the younger loads) and counts
+  //      itself in full_cnt[(t + 1) % NSLOT];
+  //   C. issues its pieces of tap t + 2 into that tap's slot once every wave has counted itself in as
+  //      having read the slot's previous tap t + 2 - NSLOT;
+  //   and after its chunk-0 MFMAs waits for full_cnt of tap t + 1 before reading it from the ring.
+  // A wave counts itself in (A, B) before it waits on anything at a tap, so the slowest wave is never
+  // blocked: no deadlock, and the waves stay within two taps of each other.  Replaces per-wave loads
+  // of each tap's fragments from L2 / L1 (16 KiB per wave-pair at C = 64, 4x the tap; timing build
+  // without them: 21.0 -> 13.5 ms for the C = 64 ParallelBlock, r06e).
+  int ring_t = 0;                    // the tap being computed
+  int ic_m = 0, ic_conv = 0, ic_j = 0;  // the next tap to issue (ring_t + 2 in the loop)
+  int dsrc[PPW];                     // per-lane source offsets of this wave's pieces
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int pc = min(wave + 8 * i, NP - 1);
+    const int pl = pc & 1, cbk = (pc >> 1) % (C / 16), ch = (pc >> 1) / (C / 16);
+    dsrc[i] = (ch * C + cbk * 16 + l15) * 128 + kg * 32 + pl * 16;
+  }
+  // members' weights and tap counts picked by uniform selects (an index into the kernel-argument
+  // arrays became a vector load that hipcc then waited for with vmcnt(0), DMA in flight included)
+  auto mpick = [&](auto a0, auto a1, auto a2, int m) { return m == 0 ? a0 : m == 1 ? a1 : a2; };
+  auto ring_issue = [&](int slot) {  // this wave's pieces of the issue cursor's tap, then advance it
+    const unsigned short* w1 = mpick(p.w1[0], p.w1[1], p.w1[2], ic_m);
+    const unsigned short* w2 = mpick(p.w2[0], p.w2[1], p.w2[2], ic_m);
+    const unsigned short* wp = (ic_conv ? w2 : w1) + (long long)ic_j * (WTAP / 2);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)wp, 0, WTAP, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = wave + 8 * i;
+      if (NP % 8 == 0 || pc < NP)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (rp_lds_t)(lds + IMG + slot * WTAP + pc * 1024), 16, dsrc[i], 0, 0, 0);
+    }
+    if (++ic_j == mpick(p.taps[0], p.taps[1], p.taps[2], ic_m)) {
+      ic_j = 0;
+      if (ic_conv == 0) ic_conv = 1;
+      else {
+        ic_conv = 0;
+        ic_m = ic_m + 1 < nmem ? ic_m + 1 : 0;
+      }
+    }
+  };
+  // the counter read is inline asm: as a C++ LDS load hipcc made it wait for the wave's LDS-DMA in
+  // flight (vmcnt(0): the pieces of tap t + 2, just issued), which it cannot tell apart from the slot
+  auto spin_ge = [&](const unsigned* c, unsigned want) {
+    const unsigned a = (unsigned)(size_t)(const __attribute__((address_space(3))) void*)c;
+    for (;;) {
+      unsigned v;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+      if (__builtin_amdgcn_readfirstlane(v) >= want) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  auto count_in = [&](unsigned* c) {  // inline asm for the same reason as spin_ge
+    const unsigned a = (unsigned)(size_t)(__attribute__((address_space(3))) void*)c;
+    if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(1u) : "memory");
+  };
+  const int wrd = lane * 16 + (2 * wc) * 2 * 1024;  // lane part of a fragment read from the ring
+  auto read_wf = [&](int slot, int ch) {
+    const char* wb = lds + IMG + slot * WTAP + wrd;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      wf[ch][cb][0] = *reinterpret_cast<const s16x8*>(wb + ((ch * (C / 16) + cb) * 2 + 0) * 1024);
+      wf[ch][cb][1] = *reinterpret_cast<const s16x8*>(wb + ((ch * (C / 16) + cb) * 2 + 1) * 1024);
+    }
   };
 
   // ---- one tap, chunk-major: the MFMAs of chunk ch for every row block of the wave, then chunk ch
@@ -807,9 +894,22 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
   // the 16-row block); a tap adds its wave-uniform row offset once, row block / chunk offsets are
   // instruction immediates
   const int pkh = (kg * NS + l15) * 16, pkl = ((4 + kg) * NS + l15) * 16;
-  auto tap = [&](f32x4 (&acc)[RB][2], int rowoff, int nrb, const unsigned short* wnext, auto hook) {
+  // RING: hook() first (its nyoung global loads are then the only ones younger than the pieces B
+  // waits for; nyoung may undercount, never overcount)
+  auto tap = [&](f32x4 (&acc)[RB][2], int rowoff, int nrb, const unsigned short* wnext, int nyoung, auto hook) {
     const int tb = (wr * 16 + rowoff) * 16;
     const char *xbh = lds + pkh + tb, *xbl = lds + pkl + tb;
+    const int t = ring_t;
+    if constexpr (RING) {
+      hook();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // A
+      count_in(rd_cnt + t % NSLOT);
+      rp_wait(nyoung);  // B
+      count_in(full_cnt + (t + 1) % NSLOT);
+      spin_ge(rd_cnt + (t + 2) % NSLOT, 8u * (unsigned)((t + 2) / NSLOT));  // C
+      ring_issue((t + 2) % NSLOT);
+      ring_t = t + 1;
+    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
@@ -830,13 +930,18 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
           }
         }
       }
-      load_wf(wnext, ch);
+      if constexpr (RING) {
+        if (ch == 0) spin_ge(full_cnt + (t + 1) % NSLOT, 8u * (unsigned)((t + 1) / NSLOT + 1));
+        read_wf((t + 1) % NSLOT, ch);
+      } else {
+        load_wf(wnext, ch);
+      }
       // keep the reloads here: left to itself the scheduler sinks all of them to the end of the tap,
       // and the next tap's first MFMAs then wait a whole L2 round trip
       __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_s_setprio(0);
-    hook();
+    if constexpr (!RING) hook();
   };
   auto no_hook = [] {};
 
@@ -847,6 +952,23 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
   auto t_shift = [&](int m, int bb) {
     return p.src_amax[m] ? h2_shift(fmaf(p.g1[m], p.src_amax[m][bb], p.bm1[m])) : 0;
   };
+  // the shifts of the tile's clip for every member, read once per tile into scalar registers (read
+  // where they are used, each load's wait took every load and DMA in flight with it)
+  // (RING: the launcher guarantees src_amax for every member, so the loads are unconditional and
+  // issued together); shs0n: member 0's S shift of the next tile's clip
+  int shs[kMaxGroup], sht[kMaxGroup], shs0n = 0;
+  auto tile_shifts = [&](int bb, int nbb) {
+    float a[kMaxGroup];
+#pragma unroll
+    for (int i = 0; i < kMaxGroup; ++i) a[i] = p.src_amax[i < nmem ? i : 0][bb];
+    const float an = p.src_amax[0][nbb];
+#pragma unroll
+    for (int i = 0; i < kMaxGroup; ++i) {
+      shs[i] = __builtin_amdgcn_readfirstlane(h2_shift(a[i]));
+      sht[i] = __builtin_amdgcn_readfirstlane(h2_shift(fmaf(p.g1[i], a[i], p.bm1[i])));
+    }
+    shs0n = __builtin_amdgcn_readfirstlane(h2_shift(an));
+  };
   int tile = blockIdx.x;
   if (tile >= total) return;  // whole workgroup, before any barrier
   int b = tile / ntl, r0 = (tile - b * ntl) * R;
@@ -854,12 +976,28 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
     const int conv = tid / (nmem * C), m = (tid / C) % nmem, c = tid % C;
     bias_lds[(conv * kMaxGroup + m) * C + c] = (conv ? p.b2[m] : p.b1[m])[c];
   }
+  if constexpr (RING) {
+    if (tid < 2 * NSLOT) rd_cnt[tid] = 0u;
+    rp_barrier();
+    ring_issue(0);
+    ring_issue(1);
+  } else {
 #pragma unroll
-  for (int ch = 0; ch < NCH; ++ch) load_wf(p.w1[0], ch);
+    for (int ch = 0; ch < NCH; ++ch) load_wf(p.w1[0], ch);
+  }
 #pragma unroll
   for (int k = 0; k < NIT; ++k) issue_fill_item(p.src[0] + (long long)b * p.bstride, r0, k);
   commit_fill(r0, __builtin_ldexpf(1.0f, s_shift(0, b)));
+  if constexpr (RING) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    count_in(full_cnt + 0);  // tap 1's pieces are counted in by B of tap 0
+  }
   rp_barrier();
+  if constexpr (RING) {
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) read_wf(0, ch);
+  }
+  wl_off = true;
   f32x4 macc[MEAN ? RB : 1][2];
 #ifdef RP_DIAG_STAMPS
   unsigned long long dg[16] = {};
@@ -868,6 +1006,7 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
     const int next_tile = tile + gridDim.x;
     const bool more = next_tile < total;
     const int nb = more ? next_tile / ntl : 0, nr0 = more ? (next_tile - nb * ntl) * R : 0;
+    if constexpr (RING) tile_shifts(b, nb);
     for (int m = 0; m < nmem; ++m) {
       const int k = p.taps[m], hk = (k - 1) >> 1, d = p.dil[m];
       const long long cb0 = (long long)b * p.bstride;
@@ -880,14 +1019,14 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
       for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int ts = p.tap_sync;
       for (int j = 0; j < k; ++j) {
-        tap(acc, G::H1 + (j - hk) * d, RB, next_tap(m, 0, j), no_hook);
+        tap(acc, G::H1 + (j - hk) * d, RB, next_tap(m, 0, j), 0, no_hook);
         if (ts && (j + 1) % ts == 0 && j + 1 < k) rp_barrier();  // workgroup-uniform
       }
       RP_T(tb);
       rp_barrier();  // every wave's S reads are done before T overwrites them
       // ---- T image: silu(c1 + b1) as h / l over the S image (zero outside the clip), range-scaled
-      const int sh_t = t_shift(m, b);
-      const float us1 = __builtin_ldexpf(1.0f, -(p.w3_shift1[m] + s_shift(m, b)));
+      const int sh_t = RING ? mpick(sht[0], sht[1], sht[2], m) : t_shift(m, b);
+      const float us1 = __builtin_ldexpf(1.0f, -(p.w3_shift1[m] + (RING ? mpick(shs[0], shs[1], shs[2], m) : s_shift(m, b))));
       const float tsc = __builtin_ldexpf(1.0f, sh_t), tlim = 65504.0f / tsc;
       float tmax = 0.f;
 #pragma unroll
@@ -906,7 +1045,7 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
             const float v = ok ? sv * tsc : 0.f;
             if (ok) tmax = fmaxf(tmax, fabsf(pre));
             unsigned short hh, ll;
-            split2h(v, hh, ll);
+            split2h_nc(v, hh, ll);
             hv[e] = (short)hh;
             lv[e] = (short)ll;
           }
@@ -927,7 +1066,9 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
       const float* nsrc = !last_m ? p.src[m + 1] + cb0 : p.src[0] + (long long)nb * p.bstride;
       const int nsr0 = !last_m ? r0 : nr0;
       f32x4 res[RB][2];
+      float dcur = 0.f;  // this clip's running max |dst| (range_report)
       auto res_hook = [&] {
+        if constexpr (!MEAN) dcur = range_cur(p.dst_amax[m], b);  // older than the residual loads
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
           const int q = min(r0 + (wr + WR * i) * 16 + l15, L - 1);
@@ -948,14 +1089,14 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
 #pragma unroll
         for (int kk = NIT / 2; kk < NIT; ++kk) issue_fill_item(nsrc, nsr0, kk);
       };
-      tap(acc, 8 - hk, nrb2, next_tap(m, 1, 0), res_hook);
+      tap(acc, 8 - hk, nrb2, next_tap(m, 1, 0), RB * 2, res_hook);
       if (ts == 1) rp_barrier();
-      tap(acc, 9 - hk, nrb2, next_tap(m, 1, 1), pf_hook0);
+      tap(acc, 9 - hk, nrb2, next_tap(m, 1, 1), has_next ? (NIT / 2) * 2 : 0, pf_hook0);
       if (ts && 2 % ts == 0) rp_barrier();
-      tap(acc, 10 - hk, nrb2, next_tap(m, 1, 2), pf_hook1);
+      tap(acc, 10 - hk, nrb2, next_tap(m, 1, 2), has_next ? (NIT - NIT / 2) * 2 : 0, pf_hook1);
       if (ts && 3 % ts == 0 && 3 < k) rp_barrier();
       for (int j = 3; j < k; ++j) {
-        tap(acc, 8 + j - hk, nrb2, next_tap(m, 1, j), no_hook);
+        tap(acc, 8 + j - hk, nrb2, next_tap(m, 1, j), 0, no_hook);
         if (ts && (j + 1) % ts == 0 && j + 1 < k) rp_barrier();
       }
       RP_T(te);
@@ -991,12 +1132,13 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
         }
       }
       if constexpr (!MEAN) {
-        if (p.dst_amax[m]) range_report(dmax, p.dst_amax[m], b, __builtin_inff(), nullptr);  // workgroup-uniform
+        if (p.dst_amax[m]) range_report(dmax, p.dst_amax[m], b, __builtin_inff(), nullptr, dcur);  // workgroup-uniform
       }
       RP_T(tf);
       if (has_next) {
         rp_barrier();  // every wave's T reads are done before the next S image overwrites them
-        commit_fill(nsr0, __builtin_ldexpf(1.0f, last_m ? s_shift(0, nb) : s_shift(m + 1, b)));
+        commit_fill(nsr0, __builtin_ldexpf(1.0f, RING ? (last_m ? shs0n : mpick(shs[1], shs[2], shs[2], m))
+                                                 : last_m ? s_shift(0, nb) : s_shift(m + 1, b)));
         rp_barrier();
       }
 #ifdef RP_DIAG_STAMPS
@@ -1014,7 +1156,9 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last tap's (unused) fragment reloads
 #ifdef RP_DIAG_STAMPS
-  (void)dg;
+  if (tid == 0)
+    for (int i = 0; i < 16; ++i) atomicAdd(&g_rp_diag[(C == 64 ? 16 : 0) + i], dg[i]);
+#endif
 #endif
 }
 
@@ -1326,19 +1470,24 @@ hipError_t launch_res_pair(const ResPairParams& p, hipStream_t s, const char** k
   q.tap_sync = std::max(0, kn.rp_sync);
   const bool mean = p.mean_out != nullptr;
   // profile names are string literals (no shared buffer between threads)
-#define DCX_RP_GO(KERN, CC, RR, NAME)                                                       \
+#define DCX_RP_GO(KERN, CC, RR, NAME, ...)                                                  \
   do {                                                                                      \
     if (kname) *kname = mean ? #KERN "<" #CC ",mean" NAME ">" : #KERN "<" #CC NAME ">";     \
-    if (mean) hipLaunchKernelGGL((KERN<CC, true, RR>), dim3(grid), dim3(w4 ? 256 : 512), 0, s, q);   \
-    else hipLaunchKernelGGL((KERN<CC, false, RR>), dim3(grid), dim3(w4 ? 256 : 512), 0, s, q);       \
+    if (mean) hipLaunchKernelGGL((KERN<CC, true, RR __VA_ARGS__>), dim3(grid), dim3(w4 ? 256 : 512), 0, s, q);   \
+    else hipLaunchKernelGGL((KERN<CC, false, RR __VA_ARGS__>), dim3(grid), dim3(w4 ? 256 : 512), 0, s, q);       \
   } while (0)
-#define DCX_RP_SIZES(KERN, CC, R0, R1, R2)                     \
+#define DCX_RP_SIZES(KERN, CC, R0, R1, R2, ...)                \
   do {                                                         \
-    if (si == 0) DCX_RP_GO(KERN, CC, R0, "");                  \
-    else if (si == 1) DCX_RP_GO(KERN, CC, R1, ",small");       \
-    else DCX_RP_GO(KERN, CC, R2, ",small");                    \
+    if (si == 0) DCX_RP_GO(KERN, CC, R0, "" __VA_ARGS__);                  \
+    else if (si == 1) DCX_RP_GO(KERN, CC, R1, ",small" __VA_ARGS__);       \
+    else DCX_RP_GO(KERN, CC, R2, ",small" __VA_ARGS__);                    \
   } while (0)
-  if (p.h3) {  // h3 weights: conv_res_pair_h3 (the barrier-free schedule at both widths)
+  bool ring_ok = kn.rp_ring != 0;  // the ring kernel reads every member's src_amax unconditionally
+  for (int m = 0; m < p.nmem; ++m) ring_ok = ring_ok && p.src_amax[m];
+  if (p.h3 && ring_ok) {  // h3 weights, the LDS weight ring (round 6, default)
+    if (p.C == 32) DCX_RP_SIZES(conv_res_pair_h3, 32, 624, 240, 112, ",ring", , true);
+    else DCX_RP_SIZES(conv_res_pair_h3, 64, 240, 112, 48, ",ring", , true);
+  } else if (p.h3) {  // h3 weights: conv_res_pair_h3 (the barrier-free schedule at both widths)
     if (p.C == 32) DCX_RP_SIZES(conv_res_pair_h3, 32, 624, 240, 112);
     else DCX_RP_SIZES(conv_res_pair_h3, 64, 240, 112, 48);
   } else if (w4) {

@@ -1,0 +1,10 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export PYTHONUNBUFFERED=1
+timeout -k 10 200 python tools/pair_bench.py > gpurun_out/r06g_pair_ring.log 2>&1 || { cat gpurun_out/r06g_pair_ring.log; exit 1; }
+DCX_RP_RING=0 timeout -k 10 200 python tools/pair_bench.py > gpurun_out/r06g_pair_noring.log 2>&1 || exit 1
+timeout -k 10 200 python tools/pair_bench.py > gpurun_out/r06g_pair_ring2.log 2>&1 || exit 1
+cat gpurun_out/r06g_pair_*.log
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_respair.py tests/test_gpu_h3.py tests/test_gpu_range.py > gpurun_out/r06g_tests.log 2>&1 || { tail -30 gpurun_out/r06g_tests.log; exit 1; }
+tail -2 gpurun_out/r06g_tests.log
+bash tools/gpu_ab_tree.sh abl_r05 > gpurun_out/r06g_ab.log 2>&1 || exit 1
