@@ -274,6 +274,33 @@ extern "C" int dcx_diag_tiles(unsigned long long* out, int max_tiles, int reset)
 // stores).  This keeps the per-element code out of the 64-way unrolled accumulator loop.
 // ---------------------------------------------------------------------------------------------
 // acc: f32x16[WR/32][WC/32] (32x32 MFMA blocks) or f32x4[WR/16][WC/16] (16x16 blocks).
+// The epilogue's per-clip range values, read before a tile's main loop so that their memory round
+// trips overlap its prologue instead of stalling the epilogue (round 6): the h2 output's shift from its
+// bound program (stored to y_ash, non-finite bounds flagged) and the clip's running max |v| (acur).
+struct EpiPre {
+  int osh;
+  float acur;
+};
+template <int RROW>
+__device__ __forceinline__ EpiPre epi_range_pre(const ConvParams& p, const ConvParams& pr, int b) {
+  EpiPre e{0, 0.f};
+  const bool h2o = (p.y6 && p.y_compact == 3) || (p.y6s && p.y6s_h2);
+  const bool h2row = (RROW & 2) && h2o && pr.yb.rowwise;
+  if (h2o && !h2row) {
+    const float bnd = range_bound(pr.yb, b);
+    e.osh = __builtin_amdgcn_readfirstlane(h2_shift(bnd));
+    if (threadIdx.x == 0) {
+      if (pr.y_ash) pr.y_ash[b] = e.osh;
+      if (pr.rflag && !(bnd <= 3.0e38f)) atomicOr(pr.rflag, RANGE_NONFINITE);
+    }
+  }
+  const bool track = pr.y_amax || (h2o && pr.rflag);
+  e.acur = track && !h2row ? __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                                                           __builtin_bit_cast(int, range_cur(pr.y_amax, b))))
+                           : 0.f;
+  return e;
+}
+
 // RROW: which per-row range forms a kernel may meet (round 6).  Bit 0: an h2 input scaled per row
 // (x_ash_row: the h3 one-tap kernels), loaded with the batch's rows; bit 1: a rowwise bound of an h2
 // output (yb.rowwise: one-tap kernels).  Tap convs pass 0, which keeps these registers out of their
@@ -282,7 +309,7 @@ extern "C" int dcx_diag_tiles(unsigned long long* out, int max_tiles, int reset)
 // kernel argument itself in grouped launches, whose private copy then leaves them out).
 template <int BM, int BN, int WM, int WN, int LDS_FLOATS, int NT, int RROW = 2, typename AccT>
 __device__ __forceinline__ void epilogue_lds(const ConvParams& p, const ConvParams& pr, AccT& acc, int q0, int co0,
-                                             int b, int ph, float* smem) {
+                                             int b, int ph, float* smem, const EpiPre* pre = nullptr) {
   constexpr int WR = BM / WM, WC = BN / WN;
   constexpr int TM = WR / 32, TN = WC / 32;
   constexpr bool M16 = sizeof(acc[0][0]) == 16;
@@ -305,7 +332,9 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, const ConvPara
   constexpr bool RIN = RROW & 1, ROUT = RROW & 2;
   const bool h2row = ROUT && h2o && pr.yb.rowwise;
   int osh = 0;
-  if (h2o && !h2row) {
+  if (pre) {
+    osh = pre->osh;
+  } else if (h2o && !h2row) {
     const float bnd = range_bound(pr.yb, b);
     osh = __builtin_amdgcn_readfirstlane(h2_shift(bnd));
     if (tid == 0) {
@@ -315,8 +344,12 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, const ConvPara
   }
   const float osc =
       __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, __builtin_ldexpf(1.0f, osh))));
+#ifdef DCX_DIAG_NORANGE  // timing build: no range tracking in the epilogues (no maxima, no flags)
+  const bool track = false;
+#else
   const bool track = pr.y_amax || (h2o && pr.rflag);
-  const float acur = track && !h2row ? range_cur(pr.y_amax, b) : 0.f;  // the clip's running max (range_report)
+#endif
+  const float acur = pre ? pre->acur : track && !h2row ? range_cur(pr.y_amax, b) : 0.f;  // the clip's running max (range_report)
   float vmax = 0.f;  // largest |v| this thread finishes (range_report)
   // Each thread finishes G consecutive output channels of a row (G = 8: 16-byte plane / compact
   // stores; the epilogue's store issue, not its bytes, sets its pace), the same channels for every
@@ -2547,6 +2580,10 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const ConvParams&
     if (tt < nsteps) dma_step(cl, ml, tt);
     adv(cl, ml);
   }
+  // the epilogue's range values and the input's unscale, in flight with the prologue's DMA
+  const EpiPre epre = epi_range_pre<HALO == 0 ? 3 : 0>(p, pr, b);
+  const float unscale = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int,
+      __builtin_ldexpf(1.0f, -(p.w3_shift + (pr.x_ash ? pr.x_ash[b] : pr.x_ash_c))))));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   seg_barrier();
   in_loop = true;
@@ -2622,12 +2659,11 @@ __device__ __forceinline__ void x3dq_tile(const ConvParams& p, const ConvParams&
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // undo the weight and the input's range scaling (powers of two: exact)
-  const float unscale = __builtin_ldexpf(1.0f, -(p.w3_shift + (pr.x_ash ? pr.x_ash[b] : pr.x_ash_c)));
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] *= unscale;
-  epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512, HALO == 0 ? 3 : 0>(p, pr, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+  epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512, HALO == 0 ? 3 : 0>(p, pr, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds), &epre);
 }
 
 template <int BN, int HALO>
@@ -2815,6 +2851,10 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const ConvParams&
     else if (SPLIT) dma_step1(cl, ml, t);
     adv(cl, ml);
   }
+  // the epilogue's range values and the input's unscale, in flight with the prologue's DMA
+  const EpiPre epre = epi_range_pre<HALO == 0 ? 3 : 0>(p, pr, b);
+  const float unscale = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int,
+      __builtin_ldexpf(1.0f, -(p.w3_shift + (pr.x_ash ? pr.x_ash[b] : pr.x_ash_c))))));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   seg_barrier();
   in_loop = true;
@@ -2898,12 +2938,11 @@ __device__ __forceinline__ void x3dw_tile(const ConvParams& p, const ConvParams&
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // undo the weight and the input's range scaling (powers of two: exact)
-  const float unscale = __builtin_ldexpf(1.0f, -(p.w3_shift + (pr.x_ash ? pr.x_ash[b] : pr.x_ash_c)));
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] *= unscale;
-  epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512, HALO == 0 ? 3 : 0>(p, pr, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds));
+  epilogue_lds<BM, BN, WM, WN, LDS_B / 4, 512, HALO == 0 ? 3 : 0>(p, pr, acc, q0, co0, b, ph, reinterpret_cast<float*>(lds), &epre);
 }
 
 template <int HALO, bool SPLIT, int BN = 256>

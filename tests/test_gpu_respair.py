@@ -126,3 +126,24 @@ def test_tile_rows_same_bits(engines, B, T):
     torch.cuda.synchronize()
     for o in h3[1:]:
         assert torch.equal(h3[0], o)
+
+
+@pytest.mark.parametrize("B,T", [(1, 1), (2, 7), (3, 40), (8, 200), (1, 93)])
+def test_ring_same_bits_as_per_wave_loads(engines, B, T):
+    """conv_res_pair_h3's LDS weight ring (round 6, the default) against its per-wave weight loads
+    (DCX_RP_RING=0): the same MFMAs in the same order on the same fragments, so the same bits, on
+    every tile height (DCX_RP_R) and over many tiles per workgroup (B=8, T=200: the tap stream and its
+    counters running on across tiles, and the issue cursor past the last tile); repeated runs of the
+    ring agree (its slot handshake has no race)."""
+    fused, _ = engines
+    z = _z(B, T, 700 + T)
+    with fused.knobs(DCX_RP_RING=0):
+        a = fused.generate(z)
+    outs = [fused.generate(z), fused.generate(z)]
+    for r in (624, 240, 112, 48):
+        with fused.knobs(DCX_RP_R=r):
+            outs.append(fused.generate(z))
+    torch.cuda.synchronize()
+    assert torch.isfinite(a).all()
+    for b in outs:
+        assert torch.equal(a, b)
