@@ -280,10 +280,11 @@ extern "C" int dcx_diag_tiles(unsigned long long* out, int max_tiles, int reset)
 struct EpiPre {
   int osh;
   float acur;
+  bool track;
 };
 template <int RROW>
 __device__ __forceinline__ EpiPre epi_range_pre(const ConvParams& p, const ConvParams& pr, int b) {
-  EpiPre e{0, 0.f};
+  EpiPre e{0, 0.f, false};
   const bool h2o = (p.y6 && p.y_compact == 3) || (p.y6s && p.y6s_h2);
   const bool h2row = (RROW & 2) && h2o && pr.yb.rowwise;
   if (h2o && !h2row) {
@@ -294,7 +295,8 @@ __device__ __forceinline__ EpiPre epi_range_pre(const ConvParams& p, const ConvP
       if (pr.rflag && !(bnd <= 3.0e38f)) atomicOr(pr.rflag, RANGE_NONFINITE);
     }
   }
-  const bool track = pr.y_amax || (h2o && pr.rflag);
+  const bool track = pr.y_amax != nullptr;
+  e.track = track;
   e.acur = track && !h2row ? __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
                                                            __builtin_bit_cast(int, range_cur(pr.y_amax, b))))
                            : 0.f;
@@ -347,7 +349,11 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, const ConvPara
 #ifdef DCX_DIAG_NORANGE  // timing build: no range tracking in the epilogues (no maxima, no flags)
   const bool track = false;
 #else
-  const bool track = pr.y_amax || (h2o && pr.rflag);
+  // the clip's max |v| where a consumer's bound needs it; an h2 output checks its values against its
+  // scale's limit only there (free: the max is taken anyway).  Elsewhere a finite value cannot pass
+  // its bound (rigorous, from measured maxima), and a non-finite bound is flagged by the bound's own
+  // evaluation (round 6: the per-element check cost ~1 VALU per element in every h2 epilogue)
+  const bool track = pre ? pre->track : pr.y_amax != nullptr;
 #endif
   const float acur = pre ? pre->acur : track && !h2row ? range_cur(pr.y_amax, b) : 0.f;  // the clip's running max (range_report)
   float vmax = 0.f;  // largest |v| this thread finishes (range_report)
@@ -607,8 +613,9 @@ __device__ __forceinline__ void epilogue_lds(const ConvParams& p, const ConvPara
     }
   }
   // (rowwise: vmax holds scaled values, and pr.y_amax is not recorded)
-  if (track) range_report(vmax, h2row ? nullptr : pr.y_amax, b, h2row ? 65504.0f : h2o ? 65504.0f / osc : __builtin_inff(),
-                          pr.rflag, acur);  // workgroup-uniform
+  if (track)  // workgroup-uniform; the staging area is free after the last pass
+    range_report_wg(vmax, h2row ? nullptr : pr.y_amax, b, h2row ? 65504.0f : h2o ? 65504.0f / osc : __builtin_inff(),
+                    pr.rflag, acur, smem, NT);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -72,6 +72,28 @@ __device__ __forceinline__ float range_bound(const RangeProg& r, long long b) {
 __device__ __forceinline__ float range_cur(const float* amax, long long b) {
   return amax ? __hip_atomic_load(amax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
 }
+// (device) range_report for a whole workgroup of nt threads (all of them call it): the waves' maxima
+// meet in LDS (barriers that leave the wave's global stores in flight) (red: nt / 64 floats the caller may overwrite, after its last LDS use) and one thread
+// reports, so a launch's first round of tiles makes one atomic per workgroup, not one per wave (the
+// atomics of all clips hit one L2 line)
+__device__ __forceinline__ void range_report_wg(float vmax, float* amax, int b, float lim, int* rflag, float cur,
+                                                float* red, int nt) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off, 64));
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = vmax;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float m = 0.f;
+  if (threadIdx.x == 0) {
+    m = red[0];
+    for (int w = 1; w < nt / 64; ++w) m = fmaxf(m, red[w]);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // red read before any wave goes on to overwrite the LDS (persistent kernels)
+  if (threadIdx.x == 0) {
+    if (amax && m > cur) atomicMax(reinterpret_cast<unsigned*>(amax + b), __float_as_uint(m));
+    if (rflag && m > lim) atomicOr(rflag, RANGE_OVER);
+  }
+}
 // (device) a wave's largest |value| (vmax >= 0 per lane) into amax[b] (atomicMax on the fp32 bits,
 // which order like the values for non-negative floats), and RANGE_OVER when it exceeds lim (the
 // largest |value| the h2 output's scale admits; +inf when there is none).  At most one atomic per

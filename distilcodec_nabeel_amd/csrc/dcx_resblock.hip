@@ -1027,8 +1027,7 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
       // ---- T image: silu(c1 + b1) as h / l over the S image (zero outside the clip), range-scaled
       const int sh_t = RING ? mpick(sht[0], sht[1], sht[2], m) : t_shift(m, b);
       const float us1 = __builtin_ldexpf(1.0f, -(p.w3_shift1[m] + (RING ? mpick(shs[0], shs[1], shs[2], m) : s_shift(m, b))));
-      const float tsc = __builtin_ldexpf(1.0f, sh_t), tlim = 65504.0f / tsc;
-      float tmax = 0.f;
+      const float tsc = __builtin_ldexpf(1.0f, sh_t);  // (rigorous bound: no per-element check, epilogue_lds)
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const int c0 = (2 * wc + cb) * 16 + 4 * (lane >> 4);
@@ -1043,7 +1042,6 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
             const float pre = acc[i][cb][e] * us1 + bias[e];
             const float sv = rp_silu(pre);
             const float v = ok ? sv * tsc : 0.f;
-            if (ok) tmax = fmaxf(tmax, fabsf(pre));
             unsigned short hh, ll;
             split2h_nc(v, hh, ll);
             hv[e] = (short)hh;
@@ -1054,7 +1052,6 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
           *reinterpret_cast<s16x4*>(dst + 4 * PS) = lv;
         }
       }
-      if (p.rflag) range_report(tmax, nullptr, b, tlim, p.rflag);  // workgroup-uniform
       rp_barrier();
       RP_T(tc);
       // ---- c2 over rows [r0, r0 + R) from the T image.  Tap 0 loads the residual rows, taps 1 and 2

@@ -219,9 +219,10 @@ int dcx_set_knob(dcx_codec* h, const char* name, int32_t value);
 int dcx_get_knob(const dcx_codec* h, const char* name, int32_t* value);
 
 /* h3 range flags (round 6; see DCX_GEMM_X6): bit 0 = an h3 operand's bound was not finite (an inf /
- * NaN upstream), bit 1 = a value exceeded its bound and saturated (never for finite inputs: the
- * bounds are rigorous).  Cumulative over the handle's calls; synchronises the device; reset != 0
- * clears them. */
+ * NaN upstream: that operand then carries inf / NaN, as the reference's fp32 would), bit 1 = a value
+ * exceeded its bound (checked where the producer takes its maxima anyway; never for finite inputs:
+ * the bounds are rigorous, from measured maxima).  Cumulative over the handle's calls; synchronises
+ * the device; reset != 0 clears them. */
 int dcx_range_flags(dcx_codec* h, int32_t* flags, int32_t reset);
 
 /* Standalone 1-D convolution primitive (the kernel family behind every stage), for tests and
