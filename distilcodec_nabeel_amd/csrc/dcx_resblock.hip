@@ -945,6 +945,9 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
   };
   auto no_hook = [] {};
 
+  // c2 computes every row block (the waves owning fewer than RB of the R output rows compute rows past
+  // them, from image rows inside the image, and drop them in the epilogue): a runtime row-block count
+  // put a branch between the MFMAs of every row block (round 6: c2 taps ran 1.2-1.6x as long as c1's)
   const int nrb2 = min(RB, (G::NB2 - wr + WR - 1) / WR);
   // range shifts (round 6): member m's S image of clip bb from the measured max |state|, its T image
   // from the bound g1 max|state| + max|b1| of c1's output (|silu(v)| <= |v|)
@@ -1086,14 +1089,14 @@ __global__ void __launch_bounds__(512, 1) conv_res_pair_h3(const ResPairParams p
 #pragma unroll
         for (int kk = NIT / 2; kk < NIT; ++kk) issue_fill_item(nsrc, nsr0, kk);
       };
-      tap(acc, 8 - hk, nrb2, next_tap(m, 1, 0), RB * 2, res_hook);
+      tap(acc, 8 - hk, RB, next_tap(m, 1, 0), RB * 2, res_hook);
       if (ts == 1) rp_barrier();
-      tap(acc, 9 - hk, nrb2, next_tap(m, 1, 1), has_next ? (NIT / 2) * 2 : 0, pf_hook0);
+      tap(acc, 9 - hk, RB, next_tap(m, 1, 1), has_next ? (NIT / 2) * 2 : 0, pf_hook0);
       if (ts && 2 % ts == 0) rp_barrier();
-      tap(acc, 10 - hk, nrb2, next_tap(m, 1, 2), has_next ? (NIT - NIT / 2) * 2 : 0, pf_hook1);
+      tap(acc, 10 - hk, RB, next_tap(m, 1, 2), has_next ? (NIT - NIT / 2) * 2 : 0, pf_hook1);
       if (ts && 3 % ts == 0 && 3 < k) rp_barrier();
       for (int j = 3; j < k; ++j) {
-        tap(acc, 8 + j - hk, nrb2, next_tap(m, 1, j), 0, no_hook);
+        tap(acc, 8 + j - hk, RB, next_tap(m, 1, j), 0, no_hook);
         if (ts && (j + 1) % ts == 0 && j + 1 < k) rp_barrier();
       }
       RP_T(te);
