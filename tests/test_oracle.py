@@ -81,7 +81,14 @@ def test_return_linear(golden):
     mel, lin = R.log_mel(torch.from_numpy(g["audio"][:1]), return_linear=True)
     assert lin.shape == m["linear_log"].shape == (1, 513, 93)
     assert np.abs(mel.numpy() - m["linear_mel"]).max() < 1e-4
-    assert np.abs(lin.numpy() - m["linear_log"]).max() < 1e-4
+    # the log of the linear magnitude: fp32 FFT rounding differs between CPUs (torch's pocketfft / MKL
+    # SIMD paths), ~1e-6 of the spectrum's peak, which the log magnifies on faint bins (measured 5e-4
+    # on a bin 60 dB under the peak); so the magnitudes are compared against the peak, the logs where
+    # the bin is within 40 dB of it
+    mag, ref = np.exp(lin.numpy().astype(np.float64)), np.exp(m["linear_log"].astype(np.float64))
+    assert np.abs(mag - ref).max() < 1e-5 * ref.max()
+    loud = ref > 1e-2 * ref.max()
+    assert np.abs(lin.numpy() - m["linear_log"])[loud].max() < 1e-4
 
 
 @pytest.mark.parametrize("name", ["e2e_batch", "e2e_3s", "e2e_real"])
