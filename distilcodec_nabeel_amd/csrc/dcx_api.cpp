@@ -142,6 +142,10 @@ struct dcx_codec {
   // only by dcx_set_knob; every launcher gets them through its parameters
   dcx::Knobs knobs;
   std::atomic<int> busy{0};
+  // a second stream for the encoder's second half-batch (stage_encode), forked from and joined to
+  // the caller's stream by events; created at dcx_finalize on the handle's device
+  hipStream_t side = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
 
   ConvW conv_pre;
   ConvW ups[8];
@@ -742,6 +746,7 @@ int* knob_slot(dcx::Knobs& k, const std::string& n) {
   if (n == "DCX_H3_SPLIT") return &k.h3_split;
   if (n == "DCX_H3_PAIRS") return &k.h3_pairs;
   if (n == "DCX_RP_RING") return &k.rp_ring;
+  if (n == "DCX_ENC_STREAMS") return &k.enc_streams;
   return nullptr;
 }
 
@@ -750,7 +755,8 @@ void knobs_from_env(dcx::Knobs& k) {
                                       "DCX_RP_W4",        "DCX_GELU_LUT",     "DCX_BF16_PERSIST", "DCX_BF16_REG_EPI",
                                       "DCX_DWCONV_TILED", "DCX_SPLIT_MIN_STEPS", "DCX_SPLIT_GROUP_OFF",
                                       "DCX_H3",           "DCX_H3_BN",        "DCX_H3_1X1",
-                                      "DCX_H3_SPLIT",     "DCX_H3_PAIRS",     "DCX_RP_RING"};
+                                      "DCX_H3_SPLIT",     "DCX_H3_PAIRS",     "DCX_RP_RING",
+                                      "DCX_ENC_STREAMS"};
   for (const char* n : names) {
     const char* e = std::getenv(n);
     if (e && *e) *knob_slot(k, n) = std::atoi(e);
@@ -1230,18 +1236,38 @@ int stage_mel(dcx_codec* h, const float* audio, int B, int64_t n, Act mel, Bump&
   return DCX_OK;
 }
 
-int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipStream_t s) {
+// Rows [r0, ...) of clip b0 on of a [B][T][C] activation in its layout (planes 3, h2 2, compact 1
+// ushorts per element), with its per-row and per-clip range pointers.
+template <class A>
+A act_rows(A a, int b0, long long r0, long long C) {
+  if (a.f) a.f += r0 * C;
+  if (a.p) a.p += r0 * C * (a.c1 ? 1 : a.h2 ? 2 : 3);
+  if (a.r.ash) a.r.ash += b0;
+  if (a.r.amax) a.r.amax += b0;
+  if (a.r.ash_row) a.r.ash_row += r0;
+  return a;
+}
+Act act_rows_out(Act a, int b0, long long r0, long long C) {
+  a = act_rows(a, b0, r0, C);
+  if (a.row_ash) a.row_ash += r0;
+  if (a.row_amax) a.row_amax += r0;
+  return a;
+}
+// A conv-input scratch region (conv_input: planes-sized) of n elements per row, from row r0 on.
+Act scratch_rows(Act a, long long r0, long long n) {
+  if (a.f) a.f += r0 * n;
+  if (a.p) a.p += r0 * n * 3;
+  if (a.row_ash) a.row_ash += r0;
+  if (a.row_amax) a.row_amax += r0;
+  return a;
+}
+
+// The encoder (encoders.py:68-76) on clips of one batch: stem conv + LN, 4 stages of (LN +
+// downsample 1x1 conv) and ConvNeXt blocks, the final LayerNorm into feat.
+int encode_clips(dcx_codec* h, const CAct& mel, int B, int T, Act feat, float* xa, float* xb, Act ln, Act hid,
+                 hipStream_t s) {
   const dcx_config& c = h->cfg;
   const long long M = (long long)B * T;
-  const int cmax = c.enc_dims[3];
-  RUN(ensure_planes(h, mel, M, c.n_mels, ws, s));
-  float* xa = ws.f((size_t)M * cmax);
-  float* xb = ws.f((size_t)M * cmax);
-  Act ln = conv_input(h, ws, (size_t)M * cmax);
-  Act hid = conv_input(h, ws, (size_t)M * 4 * cmax);
-  row_ranges(h, ws, M, ln, hid);
-  if (ws.dry) return DCX_OK;
-  if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for encode");
   ConvCall cc = framed(mel, B, T, c.n_mels);
   cc.y = xa;
   RUN(run_conv(h, h->stem, cc, s));
@@ -1260,6 +1286,42 @@ int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipSt
     for (auto& bw : h->blocks[i]) RUN(run_block(h, bw, xb, nullptr, B, T, ln, hid, s));
   }
   RUN(run_ln(h, h->enc_norm, xb, feat, M, s));  // an h2 feat: row-scaled into feat.row_ash
+  return DCX_OK;
+}
+
+// Two half-batches on two streams (round 6, Knobs::enc_streams): the encoder's launches are short
+// (the 1x1 convs of a C2 batch are 0.5-7 rounds of tiles over the CUs, e.g. pwconv2 at C = 768:
+// 354 tiles = 1.38 rounds), so one half's partly filled last round runs beside the other half's
+// launches.  Every kernel computes a clip's rows alone (tiles never span clips; per-row range
+// scales), so the halves give the bits of the whole batch.
+int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipStream_t s) {
+  const dcx_config& c = h->cfg;
+  const long long M = (long long)B * T;
+  const int cmax = c.enc_dims[3];
+  RUN(ensure_planes(h, mel, M, c.n_mels, ws, s));
+  float* xa = ws.f((size_t)M * cmax);
+  float* xb = ws.f((size_t)M * cmax);
+  Act ln = conv_input(h, ws, (size_t)M * cmax);
+  Act hid = conv_input(h, ws, (size_t)M * 4 * cmax);
+  row_ranges(h, ws, M, ln, hid);
+  if (ws.dry) return DCX_OK;
+  if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for encode");
+  if (B < 2 || !h->knobs.enc_streams || !h->side) return encode_clips(h, mel, B, T, feat, xa, xb, ln, hid, s);
+  const int B0 = (B + 1) / 2;
+  const long long r1 = (long long)B0 * T;
+  HIPCHK(h, hipEventRecord(h->fork_ev, s));
+  HIPCHK(h, hipStreamWaitEvent(h->side, h->fork_ev, 0));
+  const int rc0 = encode_clips(h, mel, B0, T, feat, xa, xb, ln, hid, s);
+  const int rc1 = rc0 != DCX_OK ? rc0
+                                : encode_clips(h, act_rows(mel, B0, r1, c.n_mels), B - B0, T,
+                                               act_rows_out(feat, B0, r1, cmax), xa + r1 * cmax, xb + r1 * cmax,
+                                               scratch_rows(ln, r1, cmax), scratch_rows(hid, r1, 4LL * cmax), h->side);
+  // joined whatever happened, so the caller's stream never runs ahead of the side stream's work
+  const hipError_t e0 = hipEventRecord(h->join_ev, h->side);
+  const hipError_t e1 = hipStreamWaitEvent(s, h->join_ev, 0);
+  RUN(rc1);
+  HIPCHK(h, e0);
+  HIPCHK(h, e1);
   return DCX_OK;
 }
 
@@ -2217,6 +2279,9 @@ void dcx_destroy(dcx_codec* h) {
   if (!h) return;
   for (void* p : h->allocs) hipFree(p);
   for (auto e : h->events) hipEventDestroy(e);
+  if (h->fork_ev) hipEventDestroy(h->fork_ev);
+  if (h->join_ev) hipEventDestroy(h->join_ev);
+  if (h->side) hipStreamDestroy(h->side);
   delete h;
 }
 
@@ -2426,6 +2491,10 @@ int dcx_finalize(dcx_codec* h, int32_t with_generator) {
   rc = build_all(h, B, with_generator);
   if (rc != DCX_OK) return rc;
   h->has_gen = with_generator != 0;
+  if (hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming) != hipSuccess)
+    return fail(h, DCX_ERR_HIP, "dcx_finalize: stream / event creation failed");
   h->finalized = true;
   h->host.clear();
   return DCX_OK;

@@ -1,0 +1,55 @@
+"""The encoder's two half-batches on two streams (Knobs::enc_streams, round 6) give the
+bits of the one-stream run: every encoder kernel computes a clip's rows alone (encoders.py:68-76:
+stem, LayerNorms, downsample convs and ConvNeXt blocks are per-frame or per-clip operations), so
+splitting the batch moves no arithmetic.  Checked on ragged-length batches (odd and even clip
+counts), in the default (h3 / x6) and the bf16 arithmetic, through the staged encoder call and the
+fused encode_decode, and with the range flags clear."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _audio(B, n, seed):
+    from distilcodec_nabeel_amd import synth
+
+    a = torch.zeros(B, n + 1)
+    for i, c in enumerate(synth.clips(B, n, seed=seed, kind="mix")):
+        a[i, 1:] = torch.from_numpy(c)
+    return a.cuda()
+
+
+@pytest.fixture(scope="module")
+def engines(cfg, state):
+    from distilcodec_nabeel_amd.engine import NativeCodec
+
+    return {"x6": NativeCodec(cfg, state, "cuda:0", gemm="x6"),
+            "bf16": NativeCodec(cfg, state, "cuda:0", gemm="bf16")}
+
+
+@pytest.mark.parametrize("mode", ["x6", "bf16"])
+@pytest.mark.parametrize("B", [2, 5])
+def test_staged_encoder_same_bits(engines, mode, B):
+    eng = engines[mode]
+    assert eng.get_knob("DCX_ENC_STREAMS") == 1  # the shipped default
+    mel = eng.mel(_audio(B, 3 * 24000 + 77, seed=B))
+    two = eng.encode(mel).clone()
+    with eng.knobs(DCX_ENC_STREAMS=0):
+        one = eng.encode(mel).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(two, one)
+    assert eng.range_flags(reset=True) == 0
+
+
+def test_encode_decode_same_bits(engines):
+    eng = engines["x6"]
+    audio = _audio(3, 2 * 24000 + 5, seed=11)
+    codes2, wav2 = [t.clone() for t in eng.encode_decode(audio)]
+    with eng.knobs(DCX_ENC_STREAMS=0):
+        codes1, wav1 = [t.clone() for t in eng.encode_decode(audio)]
+    # and a clip alone equals its row of the batch (batch invariance through the split)
+    c_alone, w_alone = [t.clone() for t in eng.encode_decode(audio[2:3])]
+    torch.cuda.synchronize()
+    assert torch.equal(codes2, codes1) and torch.equal(wav2, wav1)
+    assert torch.equal(c_alone[0], codes2[2]) and torch.equal(w_alone[0], wav2[2])
+    assert eng.range_flags(reset=True) == 0
