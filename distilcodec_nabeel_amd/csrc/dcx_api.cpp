@@ -146,6 +146,7 @@ struct dcx_codec {
   // the caller's stream by events; created at dcx_finalize on the handle's device
   hipStream_t side = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  bool no_fork = false;  // inside a whole-path half (stage_encode_decode): the encoder does not fork again
 
   ConvW conv_pre;
   ConvW ups[8];
@@ -1306,7 +1307,7 @@ int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipSt
   row_ranges(h, ws, M, ln, hid);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for encode");
-  if (B < 2 || !h->knobs.enc_streams || !h->side) return encode_clips(h, mel, B, T, feat, xa, xb, ln, hid, s);
+  if (B < 2 || !h->knobs.enc_streams || !h->side || h->no_fork) return encode_clips(h, mel, B, T, feat, xa, xb, ln, hid, s);
   const int B0 = (B + 1) / 2;
   const long long r1 = (long long)B0 * T;
   HIPCHK(h, hipEventRecord(h->fork_ev, s));
@@ -1850,8 +1851,19 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
   return DCX_OK;
 }
 
-int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int32_t* codes, float* wav, Bump& ws,
-                        hipStream_t s) {
+// conv_pre's input z of B clips x T frames: fp32, plus planes from the VQ up block's epilogue (x6)
+// unless the generator splits z.f into h2 itself with each clip's exact range (launch_h2_ranged)
+Act alloc_z(dcx_codec* h, Bump& ws, int B, int T) {
+  const long long M = (long long)B * T;
+  Act z;
+  z.f = ws.f((size_t)M * h->cfg.vq_dim);
+  if (x6_mode(h) && !(h->has_gen && takes_h3_conv(h, h->conv_pre, T))) z.p = ws.u16((size_t)M * h->cfg.vq_dim * 3);
+  return z;
+}
+
+// mel -> encoder -> VQ encode -> VQ decode of B clips, into z (the generator's input)
+int encode_clips_to_z(dcx_codec* h, const float* audio, int B, int64_t n, int32_t* codes, Act z, Bump& ws,
+                      hipStream_t s) {
   const dcx_config& c = h->cfg;
   const int T = (int)frames_of(c, n);
   const long long M = (long long)B * T;
@@ -1862,11 +1874,6 @@ int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int3
   // (reserved whenever x6 mode could write it: a dry run sees no pointers, so sizes must not depend on them)
   if (x6_mode(h)) feat.row_ash = ws.i((size_t)M);
   if (feat.h2) feat.r.ash_row = feat.row_ash;  // scaled per row by the final LayerNorm (its exact row maxima)
-  Act z;
-  z.f = ws.f((size_t)M * c.vq_dim);
-  // conv_pre's input: planes from the VQ up block's epilogue (x6), or in h3 split from z.f by the
-  // generator with each clip's exact range (launch_h2_ranged)
-  if (x6_mode(h) && !(h->has_gen && takes_h3_conv(h, h->conv_pre, T))) z.p = ws.u16((size_t)M * c.vq_dim * 3);
   const size_t mark = ws.off;
   size_t need = mark;
   auto sub = [&](auto fn) -> int {  // each sub-stage reuses the tail of the workspace
@@ -1881,11 +1888,101 @@ int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int3
   RUN(sub([&](Bump& t) { return stage_encode(h, CAct(mel), B, T, feat, t, s); }));
   RUN(sub([&](Bump& t) { return stage_vq_encode(h, CAct(feat), B, T, codes, nullptr, nullptr, nullptr, t, s); }));
   RUN(sub([&](Bump& t) { return stage_vq_decode(h, codes, B, T, z, nullptr, t, s); }));
-  // a finalized handle without generator weights can never run the generator: leave it out of
-  // the workspace size (token extraction at C3's 256 clips would otherwise reserve 139 GB)
-  if (!(ws.dry && h->finalized && !h->has_gen))
-    RUN(sub([&](Bump& t) { return stage_generate(h, CAct(z), B, T, wav, t, s); }));
+  ws.off = need;
+  return DCX_OK;
+}
+
+// a finalized handle without generator weights can never run the generator: its size is left out
+// of the workspace (token extraction at C3's 256 clips would otherwise reserve 139 GB)
+bool sizes_generator(const dcx_codec* h, const Bump& ws) { return !(ws.dry && h->finalized && !h->has_gen); }
+
+int encode_decode_clips(dcx_codec* h, const float* audio, int B, int64_t n, int32_t* codes, float* wav, Bump& ws,
+                        hipStream_t s) {
+  const int T = (int)frames_of(h->cfg, n);
+  Act z = alloc_z(h, ws, B, T);
+  const size_t mark = ws.off;
+  Bump front(ws.base, ws.cap, ws.dry);
+  front.off = mark;
+  RUN(encode_clips_to_z(h, audio, B, n, codes, z, front, s));
+  size_t need = front.off;
+  if (sizes_generator(h, ws)) {
+    Bump tail(ws.base, ws.cap, ws.dry);
+    tail.off = mark;
+    RUN(stage_generate(h, CAct(z), B, T, wav, tail, s));
+    need = std::max(need, tail.off);
+  }
   if (ws.dry) ws.off = need;
+  return DCX_OK;
+}
+
+// Half-batches on two streams (Knobs::enc_streams >= 2; 1 forks inside the encoder only): clips
+// [0, B0) on the caller's stream and [B0, B) on the side stream, each in its own part of the
+// workspace (half 0's, then half 1's: the sizes are linear in the clip count).  Every stage computes
+// a clip alone (the reference's batch semantics: clips padded to one length, no cross-clip
+// arithmetic), so the halves give the bits of the whole batch; the encoder then runs unforked inside
+// each half.  2 (default): mel -> encoder -> VQ encode -> VQ decode per half, joined, then the
+// generator on the whole batch, so the generator's long launches (the dominant kernel) run alone;
+// 3: the generator per half too.  Not in the split-K latency mode, whose partial sums share one
+// scratch region.
+int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int32_t* codes, float* wav, Bump& ws,
+                        hipStream_t s) {
+  const int mode = h->knobs.enc_streams;
+  if (B < 2 || mode < 2 || !h->side || h->split_k >= 2 || h->no_fork)
+    return encode_decode_clips(h, audio, B, n, codes, wav, ws, s);
+  struct NoFork {
+    dcx_codec* h;
+    explicit NoFork(dcx_codec* h_) : h(h_) { h->no_fork = true; }
+    ~NoFork() { h->no_fork = false; }
+  } nf(h);
+  const int B0 = (B + 1) / 2;
+  const int T = (int)frames_of(h->cfg, n);
+  Act z;
+  if (mode == 2) z = alloc_z(h, ws, B, T);
+  const size_t mark = ws.off;
+  // the halves' parts: [mark, e0) and [e0, e1) (sized by dry runs)
+  auto half = [&](int b0, int nb, Bump& w, hipStream_t st) -> int {
+    const bool dry = w.dry;
+    const float* a = dry ? nullptr : audio + (long long)b0 * n;
+    int32_t* cd = dry ? nullptr : codes + (long long)b0 * T;
+    if (mode == 2) return encode_clips_to_z(h, a, nb, n, cd, act_rows_out(z, b0, (long long)b0 * T, h->cfg.vq_dim), w, st);
+    return encode_decode_clips(h, a, nb, n, cd, dry ? nullptr : wav + (long long)b0 * T * h->cfg.hop, w, st);
+  };
+  Bump d0(nullptr, 0, true);
+  d0.off = mark;
+  RUN(half(0, B0, d0, s));
+  Bump d1(nullptr, 0, true);
+  d1.off = d0.off;
+  RUN(half(B0, B - B0, d1, s));
+  size_t need = d1.off;
+  if (mode == 2 && sizes_generator(h, ws)) {
+    Bump dg(nullptr, 0, true);
+    dg.off = mark;
+    RUN(stage_generate(h, CAct(z), B, T, nullptr, dg, s));
+    need = std::max(need, dg.off);
+  }
+  if (ws.dry) {
+    ws.off = need;
+    return DCX_OK;
+  }
+  if (need > ws.cap) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for encode_decode");
+  Bump w0(ws.base, ws.cap, false), w1(ws.base, ws.cap, false);
+  w0.off = mark;
+  w1.off = d0.off;
+  HIPCHK(h, hipEventRecord(h->fork_ev, s));
+  HIPCHK(h, hipStreamWaitEvent(h->side, h->fork_ev, 0));
+  const int rc0 = half(0, B0, w0, s);
+  const int rc1 = rc0 != DCX_OK ? rc0 : half(B0, B - B0, w1, h->side);
+  // joined whatever happened, so the caller's stream never runs ahead of the side stream's work
+  const hipError_t e0 = hipEventRecord(h->join_ev, h->side);
+  const hipError_t e1 = hipStreamWaitEvent(s, h->join_ev, 0);
+  RUN(rc1);
+  HIPCHK(h, e0);
+  HIPCHK(h, e1);
+  if (mode == 2) {
+    Bump tail(ws.base, ws.cap, false);
+    tail.off = mark;
+    RUN(stage_generate(h, CAct(z), B, T, wav, tail, s));
+  }
   return DCX_OK;
 }
 

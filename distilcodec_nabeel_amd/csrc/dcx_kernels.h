@@ -132,7 +132,7 @@ struct Knobs {
   int h3_pairs = 1;         // DCX_H3_PAIRS=0: the C = 32 / 64 ResBlock pairs in x6 arithmetic (A/B, tests)
   int h3_1x1 = 1;           // DCX_H3_1X1=0: the ConvNeXt blocks' 1x1 convs in x6 arithmetic (A/B, tests)
   int rp_ring = 1;          // DCX_RP_RING=0: conv_res_pair_h3's weights loaded per wave instead of the LDS ring (A/B)
-  int enc_streams = 1;      // DCX_ENC_STREAMS=0: the encoder's two half-batches on one stream (A/B; same bits)
+  int enc_streams = 2;      // DCX_ENC_STREAMS: half-batches on two streams, 0 off, 1 the encoder, 2 up to the generator, 3 the whole path (same bits)
 };
 
 // out[b][q*out_mul + phase][co] = epi( sum_{m<taps} sum_{ci<Cin} x[b][q + in_base[phase] + m*in_step][ci]

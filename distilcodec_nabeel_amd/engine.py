@@ -25,7 +25,7 @@ KNOB_DEFAULTS = {
     "DCX_RP_R": 0, "DCX_RP_OLD": 0, "DCX_RP_G64": 0, "DCX_RP_SYNC": 0, "DCX_RP_W4": 0, "DCX_GELU_LUT": -1,
     "DCX_BF16_PERSIST": 1, "DCX_BF16_REG_EPI": 1, "DCX_DWCONV_TILED": 0, "DCX_SPLIT_MIN_STEPS": 0,
     "DCX_SPLIT_GROUP_OFF": 0, "DCX_H3": 1, "DCX_H3_BN": 0, "DCX_H3_1X1": 1, "DCX_H3_SPLIT": 1, "DCX_H3_PAIRS": 1, "DCX_RP_RING": 1,
-    "DCX_ENC_STREAMS": 1,
+    "DCX_ENC_STREAMS": 2,
 }
 
 GEMM_MODES = {"f32": _native.DCX_GEMM_F32, "x6": _native.DCX_GEMM_X6, "bf16": _native.DCX_GEMM_BF16}

@@ -210,8 +210,10 @@ int dcx_set_split_k(dcx_codec* h, int32_t max_splits);
  * DCX_SPLIT_MIN_STEPS, DCX_SPLIT_GROUP_OFF; the h3 arithmetic of DCX_GEMM_X6 mode: DCX_H3,
  * DCX_H3_1X1, DCX_H3_PAIRS (0 = the x6 kernels for the wide generator convs, the ConvNeXt 1x1
  * convs, the small-C ResBlock pairs), DCX_H3_BN, DCX_H3_SPLIT, DCX_RP_RING (0 = per-wave weight loads in the h3
- * ResBlock pair kernel instead of its LDS ring); DCX_ENC_STREAMS (0 = the encoder's two half-batches
- * on the caller's stream alone instead of forked onto a second stream; same bits)); no launch reads the environment.  This call changes
+ * ResBlock pair kernel instead of its LDS ring); DCX_ENC_STREAMS (half-batches on the caller's stream
+ * and a second stream, same bits: 0 none, 1 the encoder, 2 (default) dcx_encode_decode up to the
+ * generator (mel, encoder, VQ encode / decode per half; the generator on the whole batch), 3 the
+ * generator per half too)); no launch reads the environment.  This call changes
  * one for later calls on this handle (a hipGraph captured earlier keeps the kernels it captured).
  * Unset, every switch selects the shipped path.  DCX_ERR_INVALID_ARG for an unknown name,
  * DCX_ERR_STATE during a stage call. */

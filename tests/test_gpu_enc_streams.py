@@ -31,7 +31,7 @@ def engines(cfg, state):
 @pytest.mark.parametrize("B", [2, 5])
 def test_staged_encoder_same_bits(engines, mode, B):
     eng = engines[mode]
-    assert eng.get_knob("DCX_ENC_STREAMS") == 1  # the shipped default
+    assert eng.get_knob("DCX_ENC_STREAMS") == 2  # the shipped default (the encoder forks at >= 1)
     mel = eng.mel(_audio(B, 3 * 24000 + 77, seed=B))
     two = eng.encode(mel).clone()
     with eng.knobs(DCX_ENC_STREAMS=0):
@@ -41,12 +41,24 @@ def test_staged_encoder_same_bits(engines, mode, B):
     assert eng.range_flags(reset=True) == 0
 
 
-def test_encode_decode_same_bits(engines):
+@pytest.mark.parametrize("B", [3, 4])
+def test_encode_decode_same_bits(engines, B):
+    """dcx_encode_decode with the half-batches forked at every level: 2 (the default: mel, encoder,
+    VQ encode / decode per half, the generator on the whole batch), 3 (the generator per half too),
+    1 (the encoder only) against one stream (0); each mode's workspace within a few % of one stream's."""
     eng = engines["x6"]
-    audio = _audio(3, 2 * 24000 + 5, seed=11)
-    codes2, wav2 = [t.clone() for t in eng.encode_decode(audio)]
+    audio = _audio(B, 2 * 24000 + 5, seed=11)
+    T = eng.num_frames(audio.shape[1])
     with eng.knobs(DCX_ENC_STREAMS=0):
         codes1, wav1 = [t.clone() for t in eng.encode_decode(audio)]
+        ws0 = eng.workspace_size(B, T)
+    for mode in (1, 3, 2):
+        with eng.knobs(DCX_ENC_STREAMS=mode):
+            codes, wav = [t.clone() for t in eng.encode_decode(audio)]
+            assert eng.workspace_size(B, T) <= ws0 * 1.1
+        torch.cuda.synchronize()
+        assert torch.equal(codes, codes1) and torch.equal(wav, wav1), mode
+    codes2, wav2 = codes, wav
     # and a clip alone equals its row of the batch (batch invariance through the split)
     c_alone, w_alone = [t.clone() for t in eng.encode_decode(audio[2:3])]
     torch.cuda.synchronize()
