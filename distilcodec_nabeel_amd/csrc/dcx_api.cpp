@@ -1851,6 +1851,13 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
   return DCX_OK;
 }
 
+// Marks a handle as inside a half-batch (stage_encode_decode): nested calls do not fork.
+struct NoFork {
+  dcx_codec* h;
+  explicit NoFork(dcx_codec* h_) : h(h_) { h->no_fork = true; }
+  ~NoFork() { h->no_fork = false; }
+};
+
 // conv_pre's input z of B clips x T frames: fp32, plus planes from the VQ up block's epilogue (x6)
 // unless the generator splits z.f into h2 itself with each clip's exact range (launch_h2_ranged)
 Act alloc_z(dcx_codec* h, Bump& ws, int B, int T) {
@@ -1929,11 +1936,7 @@ int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int3
   const int mode = h->knobs.enc_streams;
   if (B < 2 || mode < 2 || !h->side || h->split_k >= 2 || h->no_fork)
     return encode_decode_clips(h, audio, B, n, codes, wav, ws, s);
-  struct NoFork {
-    dcx_codec* h;
-    explicit NoFork(dcx_codec* h_) : h(h_) { h->no_fork = true; }
-    ~NoFork() { h->no_fork = false; }
-  } nf(h);
+  NoFork nf(h);
   const int B0 = (B + 1) / 2;
   const int T = (int)frames_of(h->cfg, n);
   Act z;

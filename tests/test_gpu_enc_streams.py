@@ -65,3 +65,4 @@ def test_encode_decode_same_bits(engines, B):
     assert torch.equal(codes2, codes1) and torch.equal(wav2, wav1)
     assert torch.equal(c_alone[0], codes2[2]) and torch.equal(w_alone[0], wav2[2])
     assert eng.range_flags(reset=True) == 0
+
