@@ -1773,7 +1773,13 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
   ra.reserve(ws, B);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for generate");
-  HIPCHK(h, dcx::launch_zero_words(ra.base, (long long)RangeArena::kSlots * B, s));
+  // the measured maxima only serve h3 consumers: none in the split-K latency mode or outside x6 mode,
+  // where the epilogues then skip their range reductions and no slot is cleared (C5: one launch and
+  // the reductions of ~40 epilogues per hop)
+#ifndef DCX_DIAG_LAT_RANGES  // A/B build: the slots tracked in every mode (round-6 first form)
+  if (!x6_mode(h) || h->split_k >= 2) ra.base = nullptr;
+#endif
+  if (ra.base) HIPCHK(h, dcx::launch_zero_words(ra.base, (long long)RangeArena::kSlots * B, s));
   // Tensors consumed by small-Cout convs are kept in fp32 (those kernels split them while
   // staging: the stages are bound by HBM traffic, and planes cost 6 B per element against 4).
   auto in_form = [&](const Act& a, const ConvW& consumer) -> Act { return fp32_form(h, a, consumer); };
