@@ -1773,7 +1773,7 @@ int stage_generate(dcx_codec* h, CAct z, int B, int T, float* wav, Bump& ws, hip
   ra.reserve(ws, B);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for generate");
-  // the measured maxima only serve h3 consumers: none in the split-K latency mode or outside x6 mode,
+  // the measured maxima only serve h3 consumers: none in the split-K latency mode or the fp32 mode,
   // where the epilogues then skip their range reductions and no slot is cleared (C5: one launch and
   // the reductions of ~40 epilogues per hop)
 #ifndef DCX_DIAG_LAT_RANGES  // A/B build: the slots tracked in every mode (round-6 first form)
