@@ -177,7 +177,7 @@ int dcx_transpose(const float* in, float* out, int32_t batch, int64_t rows, int6
  *               values (22 significant bits), three exact fp16 products per fp32 product, fp32
  *               accumulation on v_mfma_f32_16x16x32_f16 (the generator's ResBlock convs, conv_pre,
  *               the wide ConvTs, the ConvNeXt 1x1 convs).  Each h3 operand tensor is scaled per clip
- *               by a power of two chosen from a rigorous bound of its values (round 6), so the fp16
+ *               (per row for the 1x1 convs' operands) by a power of two chosen from a rigorous bound of its values (round 6), so the fp16
  *               range covers it whatever the input scale; a violated bound (only with inf / NaN
  *               inputs) saturates and sets a flag (dcx_range_flags).
  *               Both forms are held to the fp32 tolerance of the product contract (tests/test_gpu_h3.py,
