@@ -1237,7 +1237,16 @@ int stage_mel(dcx_codec* h, const float* audio, int B, int64_t n, Act mel, Bump&
   return DCX_OK;
 }
 
-// Rows [r0, ...) of clip b0 on of a [B][T][C] activation in its layout (planes 3, h2 2, compact 1
+// Whether a call may fork its half-batches onto the side stream: a handle with one, not inside a
+// half already, and a caller's stream that is not being captured into a hipGraph (a captured call
+// keeps to the caller's stream, with the same bits)
+bool may_fork(dcx_codec* h, hipStream_t s) {
+  if (!h->side || h->no_fork) return false;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusNone;
+}
+
+// Rows [r0, ...) (clips b0 on) of a [B][T][C] activation in its layout (planes 3, h2 2, compact 1
 // ushorts per element), with its per-row and per-clip range pointers.
 template <class A>
 A act_rows(A a, int b0, long long r0, long long C) {
@@ -1307,7 +1316,7 @@ int stage_encode(dcx_codec* h, CAct mel, int B, int T, Act feat, Bump& ws, hipSt
   row_ranges(h, ws, M, ln, hid);
   if (ws.dry) return DCX_OK;
   if (!ws.ok()) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for encode");
-  if (B < 2 || !h->knobs.enc_streams || !h->side || h->no_fork) return encode_clips(h, mel, B, T, feat, xa, xb, ln, hid, s);
+  if (B < 2 || !h->knobs.enc_streams || !may_fork(h, s)) return encode_clips(h, mel, B, T, feat, xa, xb, ln, hid, s);
   const int B0 = (B + 1) / 2;
   const long long r1 = (long long)B0 * T;
   HIPCHK(h, hipEventRecord(h->fork_ev, s));
@@ -1940,11 +1949,12 @@ int encode_decode_clips(dcx_codec* h, const float* audio, int B, int64_t n, int3
 int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int32_t* codes, float* wav, Bump& ws,
                         hipStream_t s) {
   const int mode = h->knobs.enc_streams;
-  if (B < 2 || mode < 2 || !h->side || h->split_k >= 2 || h->no_fork)
+  if (B < 2 || mode < 2 || h->split_k >= 2 || (!ws.dry && !may_fork(h, s)) || h->no_fork)
     return encode_decode_clips(h, audio, B, n, codes, wav, ws, s);
   NoFork nf(h);
   const int B0 = (B + 1) / 2;
   const int T = (int)frames_of(h->cfg, n);
+  const size_t start = ws.off;
   Act z;
   if (mode == 2) z = alloc_z(h, ws, B, T);
   const size_t mark = ws.off;
@@ -1969,8 +1979,11 @@ int stage_encode_decode(dcx_codec* h, const float* audio, int B, int64_t n, int3
     RUN(stage_generate(h, CAct(z), B, T, nullptr, dg, s));
     need = std::max(need, dg.off);
   }
-  if (ws.dry) {
-    ws.off = need;
+  if (ws.dry) {  // sized for the one-stream plan too (a call captured into a hipGraph does not fork)
+    Bump one(nullptr, 0, true);
+    one.off = start;
+    RUN(encode_decode_clips(h, nullptr, B, n, nullptr, nullptr, one, s));
+    ws.off = std::max(need, one.off);
     return DCX_OK;
   }
   if (need > ws.cap) return fail(h, DCX_ERR_WORKSPACE, "workspace too small for encode_decode");

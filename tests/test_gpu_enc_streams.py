@@ -66,3 +66,18 @@ def test_encode_decode_same_bits(engines, B):
     assert torch.equal(c_alone[0], codes2[2]) and torch.equal(w_alone[0], wav2[2])
     assert eng.range_flags(reset=True) == 0
 
+
+
+def test_graph_capture_keeps_one_stream(engines):
+    """A call captured into a hipGraph (the stream is capturing) does not fork; its replay gives the
+    bits of the eager call, which does (B = 2 hops of 1 s; the workspace covers both plans)."""
+    from distilcodec_nabeel_amd.streaming import GraphedHop
+
+    eng = engines["x6"]
+    hop = GraphedHop(eng, 24000, batch=2)
+    chunk = _audio(2, 24000, seed=9)[:, 1:].contiguous()
+    gc, gw = [t.clone() for t in hop(chunk)]
+    padded = torch.nn.functional.pad(chunk, (1, 0))
+    ec, ew = [t.clone() for t in eng.encode_decode(padded)]
+    torch.cuda.synchronize()
+    assert torch.equal(gc, ec) and torch.equal(gw, ew)
