@@ -438,6 +438,9 @@ def main():
             "data": "synthetic (speech/music-like 24 kHz clips; seeded synthetic weights, no checkpoint offline)",
             "config": {"workload": workload, "global_batch": n_total, "clip_samples_max": longest,
                        "frames_per_clip": frames, "parallelism": f"clip-sharded x{world}, codes all_gather",
+                       "streams": ("per GPU, two half-batches on two HIP streams up to the generator, the generator "
+                                   "on the whole shard (DCX_ENC_STREAMS=%d; same bits as one stream)"
+                                   % eng.get_knob("DCX_ENC_STREAMS")),
                        "padded_samples_per_s": round(padded / (dt / args.steps), 1)},
             "tflops_algorithmic": round(padded / 256 * MFLOP_PER_FRAME * 1e6 / (dt / args.steps) / 1e12, 1),
             "roofline": roof,
