@@ -18,6 +18,8 @@ CONFIGS = [
     {"DCX_H3_PAIRS": 0},
     {"DCX_H3_SPLIT": 0, "DCX_H3_PAIRS": 0},
     {"DCX_H3": 0, "DCX_H3_1X1": 0, "DCX_H3_PAIRS": 0},
+    {"DCX_ENC_STREAMS": 0},  # the half-batch streams (round 6): one stream, and the generator per half too
+    {"DCX_ENC_STREAMS": 3},
 ]
 
 
